@@ -1,0 +1,260 @@
+/*
+ * rt_api.h — C ABI of the MI355X-native path-tracing hot path.
+ *
+ * This is the drop-in boundary that replaces the reference's CUDA entry
+ * points for the per-pixel hot path (primary ray -> BVH traversal ->
+ * sphere/quad/AABB intersection -> material scatter -> texture eval ->
+ * multi-sample accumulation).  Everything here is plain C: fixed-width
+ * integers, doubles and pointers, no C++ or torch types.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   rt_camera_setup   <- Camera::initialize             src/core/camera/Camera.cpp:31-73
+ *   rt_scene_create   <- initialize_cuda_scene          src/scene/CudaSceneInitialization.cuh:249-300
+ *                        (+ HittableConverter::cpu_to_cuda_hittable, HittableConverter.cuh:50-111,
+ *                           MaterialConverter.cuh:26-121, TextureConverter.cuh:19-88,
+ *                           CudaSceneContext::initialize/finalize_and_upload, CudaSceneContext.cuh:71-123)
+ *   rt_scene_destroy  <- cleanup_cuda_scene             src/scene/CudaSceneInitialization.cuh:302-308
+ *   rt_render         <- cuda_init_rand_states_wrapper  src/core/camera/CameraKernelWrappers.cuh:11-13
+ *                        + cuda_static_render_wrapper   src/core/camera/CameraKernelWrappers.cuh:25-34
+ *                        + the per-batch memset/sync/D2H copy of StaticCamera::render_gpu
+ *                                                       src/core/camera/StaticCamera.cpp:235-300
+ *   rt_render_device  <- same, but accumulating raw sample sums into a caller-owned device
+ *                        buffer on a caller stream (multi-GPU sample sharding / progressive
+ *                        accumulation; the role of dynamic_render_tile_kernel's accumulation
+ *                        buffer, CameraKernels.cu:206-236)
+ *   rt_last_error     <- replaces CUDA_CHECK's exit() and the converters' exceptions
+ *                        (CudaMemoryUtility.cuh:9-15, HittableConverter.cuh:103-108): errors are
+ *                        returned as negative codes, never thrown or exit()ed across the ABI.
+ *
+ * Scene description.  The reference hands the GPU a pointer graph built from
+ * shared_ptr<Hittable> objects.  Here the caller serialises that graph into
+ * flat tables (textures, Perlin tables, materials, objects, child lists) whose
+ * entries mirror the reference classes one to one; rt_scene_create copies them,
+ * builds its own acceleration structure and uploads a device layout that the
+ * library owns.  The caller owns every pointer it passes in.
+ *
+ * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
+ * random stream is a stateless counter-based Philox4x32-10 keyed by
+ * (seed, pixel, stratum sample, bounce, slot); see DESIGN.md "RNG contract".
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define RT_OK 0
+#define RT_ERR_INVALID (-1)     /* malformed description / argument */
+#define RT_ERR_DEVICE (-2)      /* HIP runtime error (message in rt_last_error) */
+#define RT_ERR_OOM (-3)         /* device allocation failed */
+#define RT_ERR_UNSUPPORTED (-4) /* valid but not supported (e.g. nesting too deep) */
+
+typedef struct rt_vec3 {
+  double x, y, z;
+} rt_vec3;
+
+/* ---- textures (Texture.hpp:8-18) ---------------------------------------- */
+enum {
+  RT_TEX_SOLID = 0,   /* SolidColorTexture   SolidColorTexture.cpp:8-10 */
+  RT_TEX_CHECKER = 1, /* CheckerTexture      CheckerTexture.cpp:41-55   */
+  RT_TEX_NOISE = 2    /* NoiseTexture        NoiseTexture.cpp:31-34     */
+};
+
+typedef struct rt_texture_desc {
+  int32_t kind;
+  int32_t even;   /* checker: texture index used when the cell parity is even */
+  int32_t odd;    /* checker: texture index used when the parity is odd */
+  int32_t perlin; /* noise: index into rt_scene_desc.perlin */
+  double scale;   /* checker cell size / noise frequency */
+  rt_vec3 color;  /* solid colour */
+} rt_texture_desc;
+
+/* Perlin gradient + permutation tables (PerlinNoise.hpp:19-33, 150-160). */
+#define RT_PERLIN_POINTS 256
+typedef struct rt_perlin_desc {
+  rt_vec3 rand_vec[RT_PERLIN_POINTS];
+  int32_t perm_x[RT_PERLIN_POINTS];
+  int32_t perm_y[RT_PERLIN_POINTS];
+  int32_t perm_z[RT_PERLIN_POINTS];
+} rt_perlin_desc;
+
+/* ---- materials (Material.hpp:11-46) ------------------------------------- */
+enum {
+  RT_MAT_LAMBERTIAN = 0,    /* LambertianMaterial.cpp:15-59   */
+  RT_MAT_METAL = 1,         /* MetalMaterial.cpp:43-62        */
+  RT_MAT_DIELECTRIC = 2,    /* DielectricMaterial.cpp:58-85   */
+  RT_MAT_DIFFUSE_LIGHT = 3, /* DiffuseLightMaterial.cpp:12-22 */
+  RT_MAT_ISOTROPIC = 4      /* IsotropicMaterial.cpp:12-31    */
+};
+
+typedef struct rt_material_desc {
+  int32_t kind;
+  int32_t texture;         /* lambertian / diffuse_light / isotropic */
+  rt_vec3 albedo;          /* metal */
+  double fuzz;             /* metal */
+  double refraction_index; /* dielectric */
+} rt_material_desc;
+
+/* ---- hittables (Hittable.hpp:12-50) -------------------------------------- */
+enum {
+  RT_OBJ_SPHERE = 0,    /* Sphere (static / moving)   Sphere.cpp:8-28, 101-178 */
+  RT_OBJ_QUAD = 1,      /* Plane == parallelogram     Plane.cpp:6-132          */
+  RT_OBJ_LIST = 2,      /* HittableList               HittableList.cpp:26-63   */
+  RT_OBJ_ROTATE_Y = 3,  /* RotateY                    RotateY.cpp:5-103        */
+  RT_OBJ_TRANSLATE = 4, /* Translate                  Translate.cpp:7-39       */
+  RT_OBJ_MEDIUM = 5     /* ConstantMedium             ConstantMedium.cpp:25-94 */
+};
+
+typedef struct rt_object_desc {
+  int32_t kind;
+  int32_t material; /* sphere / quad: material index, -1 = none (light-list entries) */
+  int32_t child;    /* rotate_y / translate / medium: object index of the wrapped object;
+                       list: first index into rt_scene_desc.children */
+  int32_t count;    /* list: number of children */
+  rt_vec3 a;        /* sphere: centre (t=0);  quad: corner Q;  translate: offset */
+  rt_vec3 b;        /* sphere: centre at t=1 (moving only);  quad: side u */
+  rt_vec3 c;        /* quad: side v */
+  double s;         /* sphere: radius;  rotate_y: angle in degrees;  medium: density */
+  int32_t moving;   /* sphere: 1 = two-centre constructor (Sphere.cpp:15-23) */
+  int32_t phase;    /* medium: material index of the phase function (isotropic) */
+} rt_object_desc;
+
+typedef struct rt_scene_desc {
+  const rt_texture_desc *textures;
+  int32_t n_textures;
+  int32_t n_perlin;
+  const rt_perlin_desc *perlin;
+  const rt_material_desc *materials;
+  int32_t n_materials;
+  int32_t n_objects;
+  const rt_object_desc *objects;
+  const int32_t *children; /* list child tables */
+  int32_t n_children;
+  int32_t world;   /* object index of the world list (main.cpp:142 `HittableList world`) */
+  int32_t lights;  /* object index of the lights list, -1 = no lights */
+  int32_t use_bvh; /* reference -b: lights become HittableList(BVHNode(lights))
+                      (StaticCamera.cpp:35-40); the world is always traversed through
+                      the library's own BVH (closest hit is structure independent) */
+} rt_scene_desc;
+
+/* ---- camera (CameraConfig.hpp:9-35) ------------------------------------- */
+typedef struct rt_camera_desc {
+  int32_t image_width;
+  int32_t samples_per_pixel;
+  int32_t max_depth;
+  int32_t _pad0;
+  double aspect_ratio;
+  double vfov;
+  double defocus_angle;
+  double focus_dist;
+  rt_vec3 lookfrom;
+  rt_vec3 lookat;
+  rt_vec3 vup;
+  rt_vec3 background;
+} rt_camera_desc;
+
+/* The camera frame Camera::initialize derives (Camera.hpp:110-141 members);
+   exactly the arguments cuda_static_render_wrapper takes. */
+typedef struct rt_frame {
+  int32_t image_width;
+  int32_t image_height;
+  int32_t sqrt_spp; /* int(sqrt(samples_per_pixel)) (StaticCamera.cpp:74-76) */
+  int32_t max_depth;
+  rt_vec3 center;
+  rt_vec3 pixel00_loc;
+  rt_vec3 pixel_delta_u;
+  rt_vec3 pixel_delta_v;
+  rt_vec3 u, v, w;
+  rt_vec3 defocus_disk_u;
+  rt_vec3 defocus_disk_v;
+  double defocus_angle;
+  double pixel_samples_scale; /* 1/samples_per_pixel (Camera.cpp:35) */
+  rt_vec3 background;
+} rt_frame;
+
+/* ---- render ---------------------------------------------------------------- */
+enum {
+  RT_OUT_SCALED = 0, /* out = pixel_samples_scale * sum (StaticCamera.cpp:98) */
+  RT_OUT_SUM = 1     /* out = raw sum over the launched samples */
+};
+
+typedef struct rt_render_params {
+  int32_t row_begin;    /* first image row (inclusive) — StaticCamera.cpp:235 batches */
+  int32_t row_end;      /* last row (exclusive); 0,0 = whole image */
+  int32_t sample_begin; /* first linear stratum index s_j*sqrt_spp+s_i */
+  int32_t sample_count; /* number of strata; -1 = all sqrt_spp^2 */
+  uint64_t seed;        /* RNG key; replaces curand_init(time(nullptr)+pixel) */
+  int32_t output;       /* RT_OUT_SCALED / RT_OUT_SUM */
+  int32_t accumulate;   /* rt_render_device only: 1 = add into the buffer, 0 = overwrite */
+} rt_render_params;
+
+/* Per-launch traversal/shading counters (for algorithmic-bytes accounting). */
+typedef struct rt_path_stats {
+  uint64_t samples;        /* camera samples traced */
+  uint64_t segments;       /* ray segments (world traversals) */
+  uint64_t node_visits;    /* BVH node fetches */
+  uint64_t sphere_tests;   /* ray-sphere intersection tests (world traversal) */
+  uint64_t quad_tests;     /* ray-quad tests (world traversal) */
+  uint64_t other_tests;    /* instance / medium / list object visits */
+  uint64_t light_tests;    /* primitive tests done by light pdf_value */
+  uint64_t shade_events;   /* material evaluations */
+} rt_path_stats;
+
+typedef struct rt_scene_info {
+  int32_t n_nodes;     /* world BVH nodes */
+  int32_t n_leaf_refs; /* object references in BVH leaves */
+  int32_t n_spheres, n_quads, n_objects, n_light_leaves;
+  int32_t bvh_depth;
+  int32_t node_bytes;   /* bytes per BVH node in the device layout */
+  int32_t sphere_bytes; /* bytes per sphere record */
+  int32_t quad_bytes;   /* bytes per quad record */
+  int64_t device_bytes; /* total device bytes of the scene */
+} rt_scene_info;
+
+typedef struct rt_scene rt_scene; /* opaque, library-owned */
+
+int rt_abi_version(void);
+const char *rt_last_error(void); /* thread-local; valid until the next call */
+int rt_device_count(int32_t *count);
+
+int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame);
+
+int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **scene);
+int rt_scene_info_get(const rt_scene *scene, rt_scene_info *info);
+int rt_scene_destroy(rt_scene *scene);
+
+/* Render rows [row_begin,row_end) x strata [sample_begin, +sample_count) and
+   copy to host_rgb (row-major, 3 doubles per pixel, index (j-row_begin)*W+i).
+   Synchronous, like the reference's per-batch loop. */
+int rt_render(rt_scene *scene, const rt_frame *frame, const rt_render_params *params,
+              double *host_rgb);
+
+/* Same work, asynchronously on `hip_stream` (NULL = the scene's own stream),
+   writing/accumulating into a device buffer of W*(row_end-row_begin)*3 doubles. */
+int rt_render_device(rt_scene *scene, const rt_frame *frame,
+                     const rt_render_params *params, double *device_rgb,
+                     void *hip_stream);
+
+/* Run the counter-instrumented kernel variant (untimed) and return totals. */
+int rt_render_stats(rt_scene *scene, const rt_frame *frame,
+                    const rt_render_params *params, rt_path_stats *stats);
+
+/* Device time of the last render kernel launched on this scene, measured with
+   HIP events recorded on the launch stream around the kernel (ms). */
+int rt_last_kernel_ms(rt_scene *scene, double *ms);
+
+/* Quantise a device radiance buffer to 8-bit RGB on the device with the
+   reference's write_color rule (ColorUtility.hpp:11-36). */
+int rt_to_bytes_device(const double *device_rgb, int64_t n_pixels, double scale,
+                       uint8_t *device_bytes, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_API_H */

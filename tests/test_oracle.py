@@ -1,0 +1,180 @@
+"""Pin the oracle (oracle/restate.cpp) to the REAL reference.
+
+Every expected value here comes from tests/golden/*.npz, produced by
+tests/golden/make_goldens.py running the reference's own src/*.cpp
+(oracle/_ref).  Bar: bit-exact (np.array_equal), floats included.
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+from rtx import abi
+from rtx.ppm import ppm_bytes, to_bytes
+from rtx.scene import load_scene
+import oracle_lib as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SCENES = os.path.join(O.ROOT, "real-time-ray-tracing-engine_amd", "scenes")
+
+
+def _variants():
+    with open(os.path.join(GOLD, "scene_variants.json")) as f:
+        v = json.load(f)
+    for n in ("three_spheres", "cornell", "cornell_fog"):
+        with open(os.path.join(SCENES, n + ".json")) as f:
+            v[n] = json.load(f)
+    return v
+
+
+VAR = _variants()
+IMG = np.load(os.path.join(GOLD, "ref_images.npz"))
+with open(os.path.join(GOLD, "ref_images.json")) as f:
+    IMG_META = json.load(f)["cases"]
+KAT = np.load(os.path.join(GOLD, "ref_kats.npz"))
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors for philox4x32-10
+    cases = [
+        ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+        ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+        ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+         (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+    ]
+    L = O.oracle()
+    for ctr, key, want in cases:
+        c = (C.c_uint32 * 4)(*ctr)
+        k = (C.c_uint32 * 2)(*key)
+        o = (C.c_uint32 * 4)()
+        L.oracle_philox(c, k, o)
+        assert tuple(o) == want
+
+
+@pytest.mark.parametrize("case", IMG_META, ids=lambda c: c["key"] + "_" + c["scene"])
+def test_oracle_mt_matches_reference_images(case):
+    S = load_scene(VAR[case["scene"]])
+    cam = S.camera_desc(image_width=case["width"], samples_per_pixel=case["spp"],
+                        max_depth=case["depth"])
+    got = O.oracle_render(S, cam, O.MODE_MT, case["seed"], use_bvh=case["use_bvh"])
+    want = IMG[case["key"]]
+    assert got.shape == want.shape
+    assert np.array_equal(got, want, equal_nan=True), np.nanmax(np.abs(got - want))
+
+
+def test_ppm_writer_matches_reference_bytes():
+    ppm = np.load(os.path.join(GOLD, "ref_ppm.npz"))
+    S = load_scene(VAR["three_spheres"])
+    for w in (64, 400):
+        cam = S.camera_desc(image_width=w, samples_per_pixel=10, max_depth=8)
+        img = O.oracle_render(S, cam, O.MODE_MT, 42, use_bvh=0)
+        assert ppm_bytes(img) == ppm["ppm_%d" % w].tobytes()
+
+
+def test_to_byte_kat():
+    xs, want = KAT["to_byte_in"], KAT["to_byte_out"]
+    assert np.array_equal(to_bytes(xs), want)
+    L = O.oracle()
+    assert np.array_equal(np.array([L.oracle_to_byte(float(x)) for x in xs], np.uint8), want)
+
+
+def test_camera_frames_kat():
+    names = ["three_spheres", "cornell", "cornell_fog", "bouncing_static"]
+    for (ni, w), want in zip(KAT["frame_in"], KAT["frame_out"]):
+        S = load_scene(VAR[names[int(ni)]])
+        cam = S.camera_desc(image_width=int(w))
+        f = abi.Frame()
+        O.oracle().oracle_camera_setup(C.byref(cam), C.byref(f))
+        vals = [f.image_width, f.image_height, f.sqrt_spp, f.max_depth]
+        for fld in ("center", "pixel00_loc", "pixel_delta_u", "pixel_delta_v", "u", "v", "w",
+                    "defocus_disk_u", "defocus_disk_v"):
+            vals += getattr(f, fld).tolist()
+        vals += [f.defocus_angle, f.pixel_samples_scale] + f.background.tolist()
+        assert np.array_equal(np.array(vals, dtype=np.float64), want)
+
+
+def _hit_check(scene_doc, ins, outs):
+    S = load_scene(scene_doc)
+    d = S.desc()
+    L = O.oracle()
+    n_hit = 0
+    for row, want in zip(ins, outs):
+        o, hit = int(row[0]), int(row[1])
+        ray = np.ascontiguousarray(row[2:9])
+        r = np.zeros(12)
+        got = L.oracle_object_hit(C.byref(d), o, O.dptr(ray), 0.001, float("inf"), O.dptr(r))
+        assert got == hit, (o, ray)
+        if hit:
+            n_hit += 1
+            cols = list(range(11))
+            m = int(want[10])
+            if m >= 0 and d.materials[m].kind == abi.RT_MAT_ISOTROPIC:
+                cols = [0, 1, 2, 3, 4, 5, 6, 9, 10]  # ConstantMedium leaves u,v unset
+            assert np.array_equal(r[cols], want[cols]), (o, r, want)
+    return n_hit
+
+
+def test_object_hit_kat_cornell_fog():
+    # quads, lists (boxes), rotate_y, translate, constant_medium (MT draw), sphere
+    assert _hit_check(VAR["cornell_fog"], KAT["hit_cornell_fog_in"], KAT["hit_cornell_fog_out"]) > 100
+
+
+def test_object_hit_kat_spheres():
+    # static + moving spheres at random ray times
+    assert _hit_check(VAR["bouncing_noglass"], KAT["hit_spheres_in"], KAT["hit_spheres_out"]) > 100
+
+
+def test_light_pdf_kat():
+    S = load_scene(VAR["cornell_fog"])
+    d = S.desc()
+    L = O.oracle()
+    nz = 0
+    for row, want in zip(KAT["pdf_in"], KAT["pdf_out"]):
+        org = np.ascontiguousarray(row[1:4])
+        dr = np.ascontiguousarray(row[4:7])
+        got = L.oracle_object_pdf(C.byref(d), int(row[0]), O.dptr(org), O.dptr(dr))
+        assert got == want or (np.isnan(got) and np.isnan(want))
+        nz += want > 0
+    assert nz > 100
+
+
+def test_texture_kat():
+    docs = [load_scene(VAR["bouncing_noglass"]), load_scene(VAR["cornell_fog"])]
+    descs = [s.desc() for s in docs]
+    L = O.oracle()
+    for row, want in zip(KAT["tex_in"], KAT["tex_out"]):
+        d = descs[int(row[0])]
+        p = np.ascontiguousarray(row[4:7])
+        o3 = np.zeros(3)
+        L.oracle_texture_value(C.byref(d), int(row[1]), row[2], row[3], O.dptr(p), O.dptr(o3))
+        assert np.array_equal(o3, want)
+
+
+def test_counter_mode_is_sample_shardable():
+    """COUNTER mode keys every draw by (pixel, sample): rendering strata [0,k) and
+    [k,n) separately and summing equals rendering [0,n) (the multi-GPU contract)."""
+    S = load_scene(VAR["cornell_fog"])
+    cam = S.camera_desc(image_width=16, samples_per_pixel=16, max_depth=8)
+    full = O.oracle_render(S, cam, O.MODE_COUNTER, 7, samples=(0, 16), output=abi.RT_OUT_SUM)
+    a = O.oracle_render(S, cam, O.MODE_COUNTER, 7, samples=(0, 5), output=abi.RT_OUT_SUM)
+    b = O.oracle_render(S, cam, O.MODE_COUNTER, 7, samples=(5, 11), output=abi.RT_OUT_SUM)
+    np.testing.assert_allclose(a + b, full, rtol=1e-12, atol=1e-12)
+
+
+def test_counter_mode_threads_equal_serial():
+    S = load_scene(VAR["three_spheres"])
+    cam = S.camera_desc(image_width=24, samples_per_pixel=4, max_depth=8)
+    a = O.oracle_render(S, cam, O.MODE_COUNTER, 3)
+    b = O.oracle_render(S, cam, O.MODE_COUNTER, 3, threads=4)
+    assert np.array_equal(a, b)
+
+
+def test_counter_mode_statistically_matches_reference():
+    """Different random streams, same estimator: image means agree to MC error."""
+    S = load_scene(VAR["cornell"])
+    cam = S.camera_desc(image_width=20, samples_per_pixel=64, max_depth=8)
+    ref_mean = np.mean([np.nanmean(O.oracle_render(S, cam, O.MODE_MT, s)) for s in (1, 2, 3)])
+    ctr_mean = np.mean([np.nanmean(O.oracle_render(S, cam, O.MODE_COUNTER, s)) for s in (1, 2, 3)])
+    assert abs(ref_mean - ctr_mean) / ref_mean < 0.05
