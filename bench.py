@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the HIP path-tracing hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C4|C5]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+
+A step renders one full frame of the workload (every pixel x every stratum x up
+to 8 bounces).  With N ranks the frame's strata are split into N disjoint ranges
+(one per GPU, all pixels each), every rank accumulates raw fp64 sums on its own
+device, and an RCCL reduce(sum) over xGMI combines them on rank 0 — the exchange
+step of the multi-GPU path (strong scaling: the frame is fixed, N varies).
+
+Output: ONE JSON line on rank 0 (driver contract) with a roofline object (the
+render kernel's algorithmic bytes / HIP-event duration vs HBM peak) and a CPU
+baseline (the reference's own code on the host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "real-time-ray-tracing-engine_amd")
+sys.path.insert(0, PKG)
+
+BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+SCENES = os.path.join(PKG, "scenes")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# BASELINE.json configs
+CONFIGS = {
+    "C1": ("three_spheres", 400, 10, 8),
+    "C2": ("three_spheres", 1920, 64, 8),
+    "C3": ("bouncing_seed42", 1920, 256, 8),
+    "C4": ("cornell_fog", 1920, 1024, 8),
+    "C5": ("bouncing_seed42", 3840, 4096, 8),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def algorithmic_bytes(st, info, n_pixels):
+    """Bytes the kernel must fetch/store per launch under the device layout
+    (SURVEY §8d formula): node fetches x node size + primitive tests x (leaf ref
+    + item + primitive record) + light-pdf primitive tests + material/texture per
+    shading event + the fp64 accumulator store per pixel."""
+    item, ref, light_leaf, mat_tex = 32, 4, 48, 96
+    b = st["node_visits"] * info["node_bytes"]
+    b += st["sphere_tests"] * (ref + item + info["sphere_bytes"])
+    b += st["quad_tests"] * (ref + item + info["quad_bytes"])
+    b += st["other_tests"] * (ref + item + 1024)  # medium: record + boundary items
+    b += st["light_tests"] * (light_leaf + info["quad_bytes"])
+    b += (st["segments"]) * mat_tex
+    b += n_pixels * 24
+    return b
+
+
+def cpu_baseline(scene, cam_full, threads):
+    """The reference's own C++ path (oracle/_ref, built from /root/reference/src)
+    with its -p decomposition over `threads` host threads, on a bounded sample:
+    the full frame at 2x2 strata (same scene, depth, resolution)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    from rtx.scene import camera_desc  # noqa: F401
+    cam = scene.camera_desc(image_width=cam_full.image_width, samples_per_pixel=4,
+                            max_depth=cam_full.max_depth)
+    if O.ref_available():
+        t = time.time()
+        n, _ = O.ref_trace_parallel(scene, cam, threads)
+        dt = time.time() - t
+        kind = "reference"
+    else:  # reference build absent: the oracle restatement, same decomposition
+        t = time.time()
+        O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=threads)
+        dt = time.time() - t
+        n = cam.image_width * max(1, int(cam.image_width / cam.aspect_ratio)) * 4
+        kind = "port"
+    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": kind,
+            "sample": "%dx%d @ 4 spp (2x2 strata), depth %d, %s, %.1f s" % (
+                cam.image_width, max(1, int(cam.image_width / cam.aspect_ratio)),
+                cam.max_depth, scene_name_of(scene), dt)}
+
+
+def scene_name_of(scene):
+    return getattr(scene, "_name", "scene")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import torch
+    from rtx import abi
+    from rtx.render import Renderer, camera_frame
+    from rtx.scene import load_scene
+
+    if ws != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    name, width, spp, depth = CONFIGS[args.config]
+    width = args.width or width
+    spp = args.spp or spp
+    scene = load_scene(os.path.join(SCENES, name + ".json"))
+    scene._name = name
+    cam = scene.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth)
+    frame = camera_frame(cam)
+    W, H, sq = frame.image_width, frame.image_height, frame.sqrt_spp
+    n_strata = sq * sq
+    s0 = rank * n_strata // ws
+    s1 = (rank + 1) * n_strata // ws
+
+    R = Renderer(scene, device=local)
+    info = R.info()
+    acc = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(seed):
+        acc.zero_()
+        R.render_device(frame, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=(s0, s1 - s0),
+                        output=abi.RT_OUT_SUM, accumulate=1)
+        if ws > 1:
+            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+
+    for w in range(args.warmup):
+        step(1000 + w)
+    torch.cuda.synchronize(dev)
+
+    kernel_ms = []
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+        kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = W * H * n_strata  # whole frame, all ranks together
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    # roofline of the dominant (render) kernel on this rank, one launch
+    st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
+    bytes_launch = algorithmic_bytes(st, info, W * H)
+    avg_ms = sum(kernel_ms) / len(kernel_ms)
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": BASELINE["metric"],
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: JSON scene %s, seeded Philox sample stream" % name,
+        "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
+                   "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
+                   "parallelism": "stratum-shard x%d + RCCL reduce(sum)" % ws if ws > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": traffic, "kernel_ms": round(avg_ms, 3),
+                     "bytes_per_launch": int(bytes_launch),
+                     "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
+                     "counters": st},
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene, cam, min(args.cpu_threads, os.cpu_count() or 1))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    R.close()
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

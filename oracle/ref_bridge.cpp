@@ -38,8 +38,10 @@
 #include "utils/ColorUtility.hpp"
 #include "utils/math/Utility.hpp"
 
+#include <atomic>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -201,6 +203,33 @@ struct GoldenCamera : public Camera {
         o[2] = sc.z();
       }
   }
+  long long trace_parallel(HittableList &world, HittableList &lights, int threads, double *out) {
+    int sq = static_cast<int>(std::sqrt(m_samples_per_pixel));
+    for (int j = 0; j < m_image_height; ++j) {
+      std::atomic<int> next{0};
+      std::vector<std::thread> pool;
+      for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&, j]() {
+          for (;;) {
+            int i = next.fetch_add(1);
+            if (i >= m_image_width) break;
+            Color pc(0, 0, 0);
+            for (int sj = 0; sj < sq; ++sj)
+              for (int si = 0; si < sq; ++si) {
+                Ray r = get_ray(i, j, si, sj);
+                pc += ray_color(r, m_max_depth, world, lights);
+              }
+            Color sc = m_pixel_samples_scale * pc;
+            double *o = out + 3 * ((size_t)j * m_image_width + i);
+            o[0] = sc.x();
+            o[1] = sc.y();
+            o[2] = sc.z();
+          }
+        });
+      for (auto &th : pool) th.join();
+    }
+    return (long long)m_image_width * m_image_height * sq * sq;
+  }
 };
 
 void root_lists(Graph &g, const rt_scene_desc *d, HittableList &world, HittableList &lights) {
@@ -250,6 +279,27 @@ int ref_render_static(const rt_scene_desc *d, const rt_camera_desc *cam, uint32_
   StaticCamera c(make_config(cam, use_bvh != 0, parallel != 0), std::string(file));
   c.render(world, lights);
   return 0;
+}
+
+/* CPU baseline: the reference's own get_ray/ray_color over `threads` host
+   threads with the reference's -p decomposition (one task per pixel of a row,
+   a barrier per row, StaticCamera.cpp:60-100).  Each thread uses the
+   reference's thread_local engine, seeded from random_device as in the
+   reference's parallel mode, so the output is not deterministic.  Writes the
+   scaled radiance like trace(); returns the number of samples traced. */
+long long ref_trace_parallel(const rt_scene_desc *d, const rt_camera_desc *cam, int use_bvh,
+                             int threads, double *out) {
+  Graph g;
+  g.load(d);
+  HittableList world, lights;
+  root_lists(g, d, world, lights);
+  GoldenCamera c(make_config(cam, use_bvh != 0, true));
+  c.setup();
+  if (use_bvh) {
+    if (!world.get_objects().empty()) world = HittableList(std::make_shared<BVHNode>(world));
+    if (!lights.get_objects().empty()) lights = HittableList(std::make_shared<BVHNode>(lights));
+  }
+  return c.trace_parallel(world, lights, threads, out);
 }
 
 int ref_object_hit(const rt_scene_desc *d, int obj, const double ray[7], double tmin, double tmax,

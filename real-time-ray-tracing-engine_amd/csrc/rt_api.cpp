@@ -1,0 +1,381 @@
+// rt_api.cpp — implementation of include/rt_api.h on the HIP runtime.
+//
+// Ownership model (replaces the reference's singleton CudaSceneContext with its
+// __device__ d_scene_context symbol, CudaSceneContext.cuh:25-181 / .cu:9-38):
+// every rt_scene owns one device allocation holding all of its tables, a HIP
+// stream, two timing events and a lazily grown output buffer.  Nothing is global,
+// so several scenes (and several devices) coexist.  Errors never exit() or throw
+// across the ABI: they return a negative code and set a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_layout.h"
+#include "rt_scene.h"
+
+extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
+                                        double *out, unsigned long long *stats,
+                                        hipStream_t stream);
+extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double scale,
+                                          uint8_t *bytes, hipStream_t stream);
+
+struct rt_scene {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  char *block = nullptr; // all scene tables
+  size_t block_bytes = 0;
+  DScene ds;
+  rt_scene_info info;
+  double *out_buf = nullptr; // rt_render staging
+  size_t out_bytes = 0;
+  unsigned long long *stats = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string &m) {
+  g_err = m;
+  return code;
+}
+
+int hip_err(hipError_t e, const char *what) {
+  return set_err(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard { // restore the caller's current device
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int to_device_camera(const rt_frame *f, DCamera &c) {
+  if (!f) return set_err(RT_ERR_INVALID, "null frame");
+  if (f->image_width < 1 || f->image_height < 1 || f->sqrt_spp < 1 || f->max_depth < 0)
+    return set_err(RT_ERR_INVALID, "invalid frame (width/height/sqrt_spp >= 1, max_depth >= 0)");
+  auto cp = [](double *d, const rt_vec3 &v) {
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+  };
+  cp(c.center, f->center);
+  cp(c.p00, f->pixel00_loc);
+  cp(c.du, f->pixel_delta_u);
+  cp(c.dv, f->pixel_delta_v);
+  cp(c.disk_u, f->defocus_disk_u);
+  cp(c.disk_v, f->defocus_disk_v);
+  cp(c.bg, f->background);
+  c.defocus_angle = f->defocus_angle;
+  c.scale = f->pixel_samples_scale;
+  c.W = f->image_width;
+  c.H = f->image_height;
+  c.sqrt_spp = f->sqrt_spp;
+  c.max_depth = f->max_depth;
+  return RT_OK;
+}
+
+int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
+  if (!p) return set_err(RT_ERR_INVALID, "null params");
+  int r0 = p->row_begin, r1 = p->row_end;
+  if (r0 == 0 && r1 == 0) r1 = f->image_height;
+  if (r0 < 0 || r1 > f->image_height || r1 <= r0)
+    return set_err(RT_ERR_INVALID, "row range outside the image");
+  int64_t nsamp = (int64_t)f->sqrt_spp * f->sqrt_spp;
+  int sb = p->sample_begin;
+  int64_t sc = p->sample_count < 0 ? nsamp - sb : p->sample_count;
+  if (sb < 0 || sc < 0 || sb + sc > nsamp)
+    return set_err(RT_ERR_INVALID, "sample range outside [0, sqrt_spp^2)");
+  if (64 * sc > 0x7FFFFFFF) return set_err(RT_ERR_UNSUPPORTED, "too many strata in one launch");
+  if ((int64_t)f->image_width * f->image_height > 0xFFFFFFFFll)
+    return set_err(RT_ERR_UNSUPPORTED, "image too large for 32-bit pixel keys");
+  if (p->output != RT_OUT_SCALED && p->output != RT_OUT_SUM)
+    return set_err(RT_ERR_INVALID, "unknown output mode");
+  L.row_begin = r0;
+  L.row_end = r1;
+  L.sample_begin = sb;
+  L.sample_count = (int32_t)sc;
+  L.seed_lo = (uint32_t)p->seed;
+  L.seed_hi = (uint32_t)(p->seed >> 32);
+  L.output = p->output;
+  L.accumulate = p->accumulate ? 1 : 0;
+  L.tiles_x = (f->image_width + 7) / 8;
+  L.tiles_y = (r1 - r0 + 7) / 8;
+  return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char *rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(int32_t *count) {
+  if (!count) return set_err(RT_ERR_INVALID, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_err(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return RT_OK;
+}
+
+int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame) {
+  std::string err;
+  int rc = rtx::camera_setup(camera, frame, err);
+  if (rc != RT_OK) return set_err(rc, err);
+  return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
+  if (!out) return set_err(RT_ERR_INVALID, "null output pointer");
+  *out = nullptr;
+  rtx::HostScene H;
+  std::string err;
+  int rc = rtx::compile_scene(desc, H, err);
+  if (rc != RT_OK) return set_err(rc, err);
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_err(e, "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return set_err(RT_ERR_INVALID, "device index out of range");
+  DeviceGuard g(device);
+
+  // one allocation, 256-B aligned sub-ranges
+  struct Part {
+    const void *src;
+    size_t bytes;
+    size_t off;
+  };
+  std::vector<Part> parts;
+  size_t off = 0;
+  auto add = [&](const void *src, size_t bytes) {
+    parts.push_back(Part{src, bytes, off});
+    off += align256(bytes ? bytes : 1);
+    return parts.size() - 1;
+  };
+  size_t iN = add(H.nodes.data(), H.nodes.size() * sizeof(DNode));
+  size_t iR = add(H.refs.data(), H.refs.size() * sizeof(int32_t));
+  size_t iI = add(H.items.data(), H.items.size() * sizeof(DItem));
+  size_t iB = add(H.bitems.data(), H.bitems.size() * sizeof(DItem));
+  size_t iX = add(H.xforms.data(), H.xforms.size() * sizeof(DXform));
+  size_t iS = add(H.spheres.data(), H.spheres.size() * sizeof(DSphere));
+  size_t iQ = add(H.quads.data(), H.quads.size() * sizeof(DQuad));
+  size_t iM = add(H.media.data(), H.media.size() * sizeof(DMedium));
+  size_t iMa = add(H.mats.data(), H.mats.size() * sizeof(DMat));
+  size_t iTx = add(H.texs.data(), H.texs.size() * sizeof(DTex));
+  size_t iP = add(H.perlin.data(), H.perlin.size() * sizeof(DPerlin));
+  size_t iLi = add(H.lights.data(), H.lights.size() * sizeof(DLight));
+  size_t iSt = add(nullptr, 8 * sizeof(unsigned long long));
+
+  rt_scene *s = new rt_scene();
+  s->device = device;
+  s->block_bytes = off;
+  e = hipMalloc((void **)&s->block, off);
+  if (e != hipSuccess) {
+    delete s;
+    return set_err(RT_ERR_OOM, std::string("hipMalloc scene: ") + hipGetErrorString(e));
+  }
+  for (const Part &p : parts)
+    if (p.src && p.bytes) {
+      e = hipMemcpy(s->block + p.off, p.src, p.bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        (void)hipFree(s->block);
+        delete s;
+        return hip_err(e, "hipMemcpy scene");
+      }
+    }
+  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess) {
+    (void)hipFree(s->block);
+    delete s;
+    return hip_err(e, "stream/event create");
+  }
+  auto P = [&](size_t i) { return (const void *)(s->block + parts[i].off); };
+  DScene &d = s->ds;
+  d.nodes = (const DNode *)P(iN);
+  d.refs = (const int32_t *)P(iR);
+  d.items = (const DItem *)P(iI);
+  d.bitems = (const DItem *)P(iB);
+  d.xforms = (const DXform *)P(iX);
+  d.spheres = (const DSphere *)P(iS);
+  d.quads = (const DQuad *)P(iQ);
+  d.media = (const DMedium *)P(iM);
+  d.mats = (const DMat *)P(iMa);
+  d.texs = (const DTex *)P(iTx);
+  d.perlin = (const DPerlin *)P(iP);
+  d.lights = (const DLight *)P(iLi);
+  d.n_lights = (int32_t)H.lights.size();
+  d.n_nodes = (int32_t)H.nodes.size();
+  d.root_is_leaf = H.root_is_leaf;
+  d.n_root_refs = H.n_root_refs;
+  s->stats = (unsigned long long *)(s->block + parts[iSt].off);
+
+  rt_scene_info &in = s->info;
+  std::memset(&in, 0, sizeof in);
+  in.n_nodes = (int32_t)H.nodes.size();
+  in.n_leaf_refs = (int32_t)H.refs.size();
+  in.n_spheres = (int32_t)H.spheres.size();
+  in.n_quads = (int32_t)H.quads.size();
+  in.n_objects = (int32_t)H.items.size();
+  in.n_light_leaves = (int32_t)H.lights.size();
+  in.bvh_depth = H.bvh_depth;
+  in.node_bytes = (int32_t)sizeof(DNode);
+  in.sphere_bytes = (int32_t)sizeof(DSphere);
+  in.quad_bytes = (int32_t)sizeof(DQuad);
+  in.device_bytes = (int64_t)off;
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_info_get(const rt_scene *s, rt_scene_info *info) {
+  if (!s || !info) return set_err(RT_ERR_INVALID, "null argument");
+  *info = s->info;
+  return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene *s) {
+  if (!s) return RT_OK;
+  DeviceGuard g(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->out_buf) (void)hipFree(s->out_buf);
+  if (s->block) (void)hipFree(s->block);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  return RT_OK;
+}
+
+static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_out,
+                  unsigned long long *stats, hipStream_t st) {
+  hipError_t e = hipEventRecord(s->ev0, st);
+  if (e != hipSuccess) return hip_err(e, "hipEventRecord");
+  e = rtk_launch_render(&s->ds, &C, &L, dev_out, stats, st);
+  if (e != hipSuccess) return hip_err(e, "render kernel launch");
+  e = hipEventRecord(s->ev1, st);
+  if (e != hipSuccess) return hip_err(e, "hipEventRecord");
+  s->timed = true;
+  return RT_OK;
+}
+
+static int ensure_out(rt_scene *s, size_t bytes) {
+  if (s->out_bytes >= bytes) return RT_OK;
+  if (s->out_buf) {
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipFree(s->out_buf);
+    s->out_buf = nullptr;
+    s->out_bytes = 0;
+  }
+  hipError_t e = hipMalloc((void **)&s->out_buf, bytes);
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc output: ") + hipGetErrorString(e));
+  s->out_bytes = bytes;
+  return RT_OK;
+}
+
+int rt_render(rt_scene *s, const rt_frame *f, const rt_render_params *p, double *host_rgb) {
+  if (!s || !host_rgb) return set_err(RT_ERR_INVALID, "null argument");
+  DCamera C;
+  DLaunch L;
+  int rc = to_device_camera(f, C);
+  if (rc) return rc;
+  if ((rc = to_launch(f, p, L))) return rc;
+  DeviceGuard g(s->device);
+  rt_render_params q = *p;
+  q.accumulate = 0;
+  L.accumulate = 0;
+  size_t n = (size_t)f->image_width * (L.row_end - L.row_begin) * 3;
+  if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
+  if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream))) return rc;
+  hipError_t e = hipMemcpyAsync(host_rgb, s->out_buf, n * sizeof(double), hipMemcpyDeviceToHost,
+                                s->stream);
+  if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync D2H");
+  e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return hip_err(e, "render kernel");
+  return RT_OK;
+}
+
+int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, double *dev_rgb,
+                     void *hip_stream) {
+  if (!s || !dev_rgb) return set_err(RT_ERR_INVALID, "null argument");
+  DCamera C;
+  DLaunch L;
+  int rc = to_device_camera(f, C);
+  if (rc) return rc;
+  if ((rc = to_launch(f, p, L))) return rc;
+  DeviceGuard g(s->device);
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->stream;
+  return launch(s, C, L, dev_rgb, nullptr, st);
+}
+
+int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
+                    rt_path_stats *stats) {
+  if (!s || !stats) return set_err(RT_ERR_INVALID, "null argument");
+  DCamera C;
+  DLaunch L;
+  int rc = to_device_camera(f, C);
+  if (rc) return rc;
+  if ((rc = to_launch(f, p, L))) return rc;
+  DeviceGuard g(s->device);
+  L.accumulate = 0;
+  size_t n = (size_t)f->image_width * (L.row_end - L.row_begin) * 3;
+  if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
+  hipError_t e = hipMemsetAsync(s->stats, 0, 8 * sizeof(unsigned long long), s->stream);
+  if (e != hipSuccess) return hip_err(e, "hipMemsetAsync stats");
+  if ((rc = launch(s, C, L, s->out_buf, s->stats, s->stream))) return rc;
+  unsigned long long h[8];
+  e = hipMemcpyAsync(h, s->stats, sizeof h, hipMemcpyDeviceToHost, s->stream);
+  if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync stats");
+  e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return hip_err(e, "stats kernel");
+  stats->samples = h[0];
+  stats->segments = h[1];
+  stats->node_visits = h[2];
+  stats->sphere_tests = h[3];
+  stats->quad_tests = h[4];
+  stats->other_tests = h[5];
+  stats->light_tests = h[6];
+  stats->shade_events = h[7];
+  return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_scene *s, double *ms) {
+  if (!s || !ms) return set_err(RT_ERR_INVALID, "null argument");
+  if (!s->timed) return set_err(RT_ERR_INVALID, "no kernel launched yet");
+  DeviceGuard g(s->device);
+  hipError_t e = hipEventSynchronize(s->ev1);
+  if (e != hipSuccess) return hip_err(e, "hipEventSynchronize");
+  float t = 0;
+  e = hipEventElapsedTime(&t, s->ev0, s->ev1);
+  if (e != hipSuccess) return hip_err(e, "hipEventElapsedTime");
+  *ms = t;
+  return RT_OK;
+}
+
+int rt_to_bytes_device(const double *rgb, int64_t n, double scale, uint8_t *bytes,
+                       void *hip_stream) {
+  if (!rgb || !bytes || n < 0) return set_err(RT_ERR_INVALID, "invalid argument");
+  hipError_t e = rtk_launch_to_bytes(rgb, n, scale, bytes, (hipStream_t)hip_stream);
+  if (e != hipSuccess) return hip_err(e, "to_bytes launch");
+  return RT_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,143 @@
+// rt_layout.h — device-side scene layout shared by the host scene compiler
+// (rt_scene.cpp) and the HIP kernels (rt_kernel.hip).
+//
+// Replaces the reference's pointer graph of 256-B sub-allocated CudaHittable /
+// CudaSphere / CudaPlane / CudaBVHNode structs (CudaSceneContext.cuh:150-172,
+// Hittable.cuh:37-49, BVHNode.cuh:16-22) with flat index-linked arrays.
+//
+// The object graph is flattened at scene-compile time into leaf ITEMS: a sphere,
+// a quad or a constant medium, each with the chain of RotateY/Translate
+// transforms above it (outermost first).  Lists disappear: closest hit over
+// List(A,B) is closest hit over {A,B}, and Rot(List(A,B)) hits exactly like
+// {Rot(A),Rot(B)} because every member sees the identical transformed ray.  A
+// medium keeps its boundary as a range of items in the medium's local frame.
+// The device code therefore needs no recursion and no function calls.
+//
+//   - world BVH: binary nodes carrying BOTH children's boxes (one 128-B fetch
+//     tests two boxes), children by index, leaves as ranges of item references;
+//   - lights: flattened to weighted leaves (primitive + transform chain), so light
+//     sampling and the light pdf are plain loops.
+// Everything is fp64, matching the reference arithmetic (Vec3.hpp:184).
+#ifndef RT_LAYOUT_H
+#define RT_LAYOUT_H
+#include <stdint.h>
+
+#define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
+#define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
+
+enum DItemKind {
+  I_SPHERE = 0,
+  I_QUAD = 1,
+  I_MEDIUM = 2,
+  I_NONE = 3 // lights only: Hittable::pdf_value 0, random (1,0,0)
+};
+
+struct DItem {       // 32 B
+  int32_t kind;
+  int32_t idx;       // index into spheres / quads / media
+  int32_t xf_first;  // transform chain in xforms[], outermost first
+  int32_t xf_count;
+  int32_t mat;       // primitive material (-1 for light-only primitives)
+  int32_t id;        // caller's object index (medium RNG key)
+  int32_t pad[2];
+};
+
+enum DXformKind { X_TRANSLATE = 0, X_ROTATE_Y = 1 };
+struct DXform {      // 32 B — Translate offset or RotateY (sin, cos)
+  int32_t kind, pad;
+  double a, b, c;    // translate: offset xyz; rotate: a = sin, b = cos
+};
+
+struct DSphere {     // 64 B — Sphere.hpp: m_center Ray (c0, c1-c0), m_radius
+  double c0[3];
+  double dir[3];     // c1 - c0, 0 for static spheres
+  double r;
+  double rr;         // r*r, as Sphere::hit computes it
+};
+
+struct DQuad {       // 144 B — Plane.hpp members
+  double Q[3], u[3], v[3];
+  double n[3];       // unit normal
+  double w[3];       // n / (n.n)
+  double D;
+  double area;
+  double pad;
+};
+
+struct DMedium {     // ConstantMedium: -1/density, phase material, boundary items
+  double neg_inv_density;
+  int32_t phase, id;
+  int32_t b_first, b_count; // boundary items in bitems[] (medium-local frame)
+};
+
+struct DNode {       // 128 B: both children's boxes + links
+  double lo[2][3];
+  double hi[2][3];
+  int32_t child[2];  // >= 0 inner node index; < 0: leaf, refs at ~child
+  int32_t count[2];  // leaf ref count, 0 for inner children
+  int32_t pad[4];
+};
+
+struct DMat {        // 48 B
+  int32_t kind, tex;
+  double albedo[3];
+  double fuzz;
+  double ior;
+};
+
+struct DTex {        // 48 B
+  int32_t kind, even, odd, perlin;
+  double scale;
+  double color[3];
+  double pad;
+};
+
+struct DPerlin {
+  double rv[256][3];
+  int32_t px[256], py[256], pz[256];
+};
+
+struct DLight {      // flattened light leaf (48 B)
+  int32_t kind;      // I_SPHERE / I_QUAD / I_NONE
+  int32_t idx;
+  int32_t xf_first, xf_count;
+  double weight;     // product of 1/N over the list / BVH levels above it
+  double cum;        // cumulative weight in DFS order (selection)
+  double pad[2];
+};
+
+struct DScene {      // kernel argument (by value)
+  const DNode *nodes;
+  const int32_t *refs;   // leaf item references
+  const DItem *items;    // world items
+  const DItem *bitems;   // medium boundary items
+  const DXform *xforms;
+  const DSphere *spheres;
+  const DQuad *quads;
+  const DMedium *media;
+  const DMat *mats;
+  const DTex *texs;
+  const DPerlin *perlin;
+  const DLight *lights;
+  int32_t n_lights;
+  int32_t n_nodes;
+  int32_t root_is_leaf;  // whole world is one leaf: refs [0, n_root_refs)
+  int32_t n_root_refs;
+};
+
+struct DCamera {     // the rt_frame values the kernel needs
+  double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
+  double defocus_angle;
+  double scale;
+  int32_t W, H, sqrt_spp, max_depth;
+};
+
+struct DLaunch {
+  int32_t row_begin, row_end;
+  int32_t sample_begin, sample_count;
+  uint32_t seed_lo, seed_hi;
+  int32_t output, accumulate;
+  int32_t tiles_x, tiles_y;
+};
+
+#endif

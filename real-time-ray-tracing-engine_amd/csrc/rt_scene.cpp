@@ -1,0 +1,888 @@
+// rt_scene.cpp — host scene compiler for the HIP path tracer.
+//
+// Takes the caller's flat rt_scene_desc (one entry per reference object, see
+// include/rt_api.h), validates it, derives the per-object data the reference
+// computes in its constructors (Plane.cpp:6-21, Sphere.cpp:8-23, RotateY.cpp:5-35,
+// Translate.cpp:7-10, ConstantMedium.cpp:7-21), computes the reference's bounding
+// boxes (AABB.cpp:7-27, 167-175), builds a binned-SAH BVH over the world's top-level
+// objects and flattens the light list into weighted leaves.
+//
+// The world BVH is the library's own: closest-hit results do not depend on the
+// tree shape.  The LIGHT tree, however, changes the light pdf weights when the
+// reference runs with -b (lights = HittableList(BVHNode(lights)),
+// StaticCamera.cpp:35-40; BVHNode::pdf_value/random, BVHNode.cpp:149-166), so for
+// use_bvh the light list is split exactly as BVHNode's constructor splits it
+// (BVHNode.cpp:21-123) and each leaf carries the product of the 1/2 and 1/N
+// weights above it.
+#include "rt_scene.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <limits>
+
+namespace rtx {
+namespace {
+
+const double kInf = std::numeric_limits<double>::infinity();
+const double kPi = 3.1415926535897932385;
+
+struct P3 {
+  double x, y, z;
+};
+inline P3 p3(const rt_vec3 &v) { return P3{v.x, v.y, v.z}; }
+inline P3 add(P3 a, P3 b) { return P3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline P3 sub(P3 a, P3 b) { return P3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline P3 scl(double t, P3 a) { return P3{t * a.x, t * a.y, t * a.z}; }
+inline double dotp(P3 a, P3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline P3 crossp(P3 a, P3 b) {
+  return P3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+inline double comp(P3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+// Axis-aligned box with the reference's interval semantics.
+struct Bx {
+  double lo[3], hi[3];
+};
+Bx bx_empty() {
+  Bx b;
+  for (int i = 0; i < 3; ++i) {
+    b.lo[i] = kInf;
+    b.hi[i] = -kInf;
+  }
+  return b;
+}
+void bx_pad(Bx &b) { // pad_to_minimums: intervals narrower than 1e-4 grow by 1e-4
+  for (int i = 0; i < 3; ++i)
+    if (b.hi[i] - b.lo[i] < 0.0001) {
+      b.lo[i] -= 0.0001 * 0.5;
+      b.hi[i] += 0.0001 * 0.5;
+    }
+}
+Bx bx_points(P3 a, P3 b) {
+  Bx r;
+  for (int i = 0; i < 3; ++i) {
+    double u = comp(a, i), v = comp(b, i);
+    r.lo[i] = u <= v ? u : v;
+    r.hi[i] = u <= v ? v : u;
+  }
+  bx_pad(r);
+  return r;
+}
+Bx bx_join(const Bx &a, const Bx &b) {
+  Bx r;
+  for (int i = 0; i < 3; ++i) {
+    r.lo[i] = a.lo[i] <= b.lo[i] ? a.lo[i] : b.lo[i];
+    r.hi[i] = a.hi[i] >= b.hi[i] ? a.hi[i] : b.hi[i];
+  }
+  return r;
+}
+double bx_area(const Bx &b) {
+  double d[3];
+  for (int i = 0; i < 3; ++i) d[i] = b.hi[i] - b.lo[i];
+  return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+}
+P3 bx_center(const Bx &b) {
+  return P3{(b.lo[0] + b.hi[0]) * 0.5, (b.lo[1] + b.hi[1]) * 0.5, (b.lo[2] + b.hi[2]) * 0.5};
+}
+int bx_longest(const Bx &b) {
+  double sx = b.hi[0] - b.lo[0], sy = b.hi[1] - b.lo[1], sz = b.hi[2] - b.lo[2];
+  if (sx > sy) return sx > sz ? 0 : 2;
+  return sy > sz ? 1 : 2;
+}
+
+struct Compiler {
+  const rt_scene_desc *D;
+  HostScene &H;
+  std::string &err;
+  std::vector<Bx> box;
+  std::vector<int> state; // 0 unvisited, 1 in progress, 2 done
+  std::vector<int> depth; // composite nesting depth of each object
+
+  Compiler(const rt_scene_desc *d, HostScene &h, std::string &e) : D(d), H(h), err(e) {}
+
+  bool fail(const std::string &m) {
+    err = m;
+    return false;
+  }
+
+  bool check_texture(int t, int hops) {
+    if (t < 0 || t >= D->n_textures) return fail("texture index out of range");
+    if (hops > 64) return fail("checker texture cycle");
+    const rt_texture_desc &x = D->textures[t];
+    if (x.kind == RT_TEX_CHECKER) {
+      if (!(x.scale != 0)) return fail("checker scale must be non-zero");
+      return check_texture(x.even, hops + 1) && check_texture(x.odd, hops + 1);
+    }
+    if (x.kind == RT_TEX_NOISE) {
+      if (x.perlin < 0 || x.perlin >= D->n_perlin) return fail("noise texture perlin index out of range");
+      return true;
+    }
+    if (x.kind != RT_TEX_SOLID) return fail("unknown texture kind");
+    return true;
+  }
+
+  bool check_material(int m, bool allow_none) {
+    if (m < 0) return allow_none ? true : fail("world primitive without material");
+    if (m >= D->n_materials) return fail("material index out of range");
+    const rt_material_desc &x = D->materials[m];
+    switch (x.kind) {
+    case RT_MAT_LAMBERTIAN:
+    case RT_MAT_DIFFUSE_LIGHT:
+    case RT_MAT_ISOTROPIC:
+      return check_texture(x.texture, 0);
+    case RT_MAT_METAL:
+    case RT_MAT_DIELECTRIC:
+      return true;
+    }
+    return fail("unknown material kind");
+  }
+
+  // Visit object o: compute its box (reference rules) and nesting depth.
+  bool visit(int o) {
+    if (o < 0 || o >= D->n_objects) return fail("object index out of range");
+    if (state[o] == 2) return true;
+    if (state[o] == 1) return fail("object graph has a cycle");
+    state[o] = 1;
+    const rt_object_desc &x = D->objects[o];
+    Bx b = bx_empty();
+    int dep = 0;
+    switch (x.kind) {
+    case RT_OBJ_SPHERE: {
+      P3 rv{x.s, x.s, x.s};
+      P3 c0 = p3(x.a);
+      if (x.moving) { // Sphere.cpp:15-23
+        P3 dir = sub(p3(x.b), c0);
+        P3 a0 = add(c0, scl(0, dir)), a1 = add(c0, scl(1, dir));
+        b = bx_join(bx_points(sub(a0, rv), add(a0, rv)), bx_points(sub(a1, rv), add(a1, rv)));
+      } else {
+        b = bx_points(sub(c0, rv), add(c0, rv));
+      }
+      if (!(x.s >= 0) && !(x.s < 0)) return fail("sphere radius is NaN");
+      break;
+    }
+    case RT_OBJ_QUAD: { // Plane.cpp:17-20
+      P3 Q = p3(x.a), u = p3(x.b), v = p3(x.c);
+      b = bx_join(bx_points(Q, add(add(Q, u), v)), bx_points(add(Q, u), add(Q, v)));
+      break;
+    }
+    case RT_OBJ_LIST: {
+      if (x.count < 0 || x.child < 0 || x.child + x.count > D->n_children)
+        return fail("list child range out of bounds");
+      for (int k = 0; k < x.count; ++k) {
+        int c = D->children[x.child + k];
+        if (!visit(c)) return false;
+        b = bx_join(b, box[c]);
+        dep = std::max(dep, depth[c] + 1);
+      }
+      break;
+    }
+    case RT_OBJ_ROTATE_Y: { // RotateY.cpp:5-35
+      if (!visit(x.child)) return false;
+      double rad = x.s * kPi / 180.0;
+      double s = std::sin(rad), c = std::cos(rad);
+      const Bx &cb = box[x.child];
+      double mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+      for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+          for (int k = 0; k < 2; k++) {
+            double px = i * cb.hi[0] + (1 - i) * cb.lo[0];
+            double py = j * cb.hi[1] + (1 - j) * cb.lo[1];
+            double pz = k * cb.hi[2] + (1 - k) * cb.lo[2];
+            double t[3] = {c * px + s * pz, py, -s * px + c * pz};
+            for (int a = 0; a < 3; a++) {
+              mn[a] = std::fmin(mn[a], t[a]);
+              mx[a] = std::fmax(mx[a], t[a]);
+            }
+          }
+      b = bx_points(P3{mn[0], mn[1], mn[2]}, P3{mx[0], mx[1], mx[2]});
+      dep = depth[x.child] + 1;
+      break;
+    }
+    case RT_OBJ_TRANSLATE: { // Translate.cpp:7-10 + AABBUtility.hpp:7-11
+      if (!visit(x.child)) return false;
+      const Bx &cb = box[x.child];
+      double off[3] = {x.a.x, x.a.y, x.a.z};
+      for (int i = 0; i < 3; ++i) {
+        b.lo[i] = cb.lo[i] + off[i];
+        b.hi[i] = cb.hi[i] + off[i];
+      }
+      bx_pad(b);
+      dep = depth[x.child] + 1;
+      break;
+    }
+    case RT_OBJ_MEDIUM: {
+      if (!visit(x.child)) return false;
+      if (!(x.s > 0)) return fail("medium density must be > 0");
+      if (!check_material(x.phase, false)) return false;
+      if (D->materials[x.phase].kind != RT_MAT_ISOTROPIC)
+        return fail("medium phase function must be an isotropic material");
+      b = box[x.child];
+      dep = depth[x.child] + 1;
+      break;
+    }
+    default:
+      return fail("unknown object kind");
+    }
+    box[o] = b;
+    depth[o] = dep;
+    state[o] = 2;
+    return true;
+  }
+
+  // World primitives must carry a material (a null MaterialPtr would crash the
+  // reference at record.material->emitted, Camera.cpp:248).
+  bool check_world_materials(int o) {
+    const rt_object_desc &x = D->objects[o];
+    switch (x.kind) {
+    case RT_OBJ_SPHERE:
+    case RT_OBJ_QUAD:
+      return check_material(x.material, false);
+    case RT_OBJ_LIST:
+      for (int k = 0; k < x.count; ++k)
+        if (!check_world_materials(D->children[x.child + k])) return false;
+      return true;
+    case RT_OBJ_ROTATE_Y:
+    case RT_OBJ_TRANSLATE:
+      return check_world_materials(x.child);
+    case RT_OBJ_MEDIUM:
+      return true; // boundary materials are never read (ConstantMedium.cpp:88-91)
+    }
+    return true;
+  }
+
+  // ------------------------------------------------------------ flattening
+  // The graph below each world object becomes leaf items: primitive or medium +
+  // its chain of RotateY/Translate objects (outermost first).  Lists vanish.
+  struct FItem {
+    int kind; // I_SPHERE / I_QUAD / I_MEDIUM
+    int obj;
+    std::vector<int> chain;
+  };
+  std::vector<int> sphere_of, quad_of;
+
+  bool flatten(int o, std::vector<int> &chain, std::vector<FItem> &out, bool in_boundary) {
+    const rt_object_desc &x = D->objects[o];
+    switch (x.kind) {
+    case RT_OBJ_SPHERE:
+      out.push_back(FItem{I_SPHERE, o, chain});
+      return true;
+    case RT_OBJ_QUAD:
+      out.push_back(FItem{I_QUAD, o, chain});
+      return true;
+    case RT_OBJ_LIST:
+      for (int k = 0; k < x.count; ++k)
+        if (!flatten(D->children[x.child + k], chain, out, in_boundary)) return false;
+      return true;
+    case RT_OBJ_ROTATE_Y:
+    case RT_OBJ_TRANSLATE: {
+      if ((int)chain.size() >= RT_MAX_CHAIN)
+        return fail("UNSUPPORTED: more than RT_MAX_CHAIN nested rotate_y/translate");
+      chain.push_back(o);
+      bool ok = flatten(x.child, chain, out, in_boundary);
+      chain.pop_back();
+      return ok;
+    }
+    case RT_OBJ_MEDIUM:
+      if (in_boundary) return fail("UNSUPPORTED: constant_medium inside a medium boundary");
+      out.push_back(FItem{I_MEDIUM, o, chain});
+      return true;
+    }
+    return fail("unknown object kind");
+  }
+
+  int sphere_record(int o) {
+    if (sphere_of[o] >= 0) return sphere_of[o];
+    const rt_object_desc &x = D->objects[o];
+    DSphere s;
+    P3 c0 = p3(x.a);
+    P3 dir = x.moving ? sub(p3(x.b), c0) : P3{0, 0, 0}; // Sphere.cpp:15-23: m_center = Ray(c0, c1-c0)
+    s.c0[0] = c0.x, s.c0[1] = c0.y, s.c0[2] = c0.z;
+    s.dir[0] = dir.x, s.dir[1] = dir.y, s.dir[2] = dir.z;
+    s.r = std::fmax(0, x.s);
+    s.rr = s.r * s.r;
+    sphere_of[o] = (int)H.spheres.size();
+    H.spheres.push_back(s);
+    return sphere_of[o];
+  }
+
+  int quad_record(int o) { // Plane.cpp:6-16
+    if (quad_of[o] >= 0) return quad_of[o];
+    const rt_object_desc &x = D->objects[o];
+    DQuad q;
+    std::memset(&q, 0, sizeof q);
+    P3 Q = p3(x.a), u = p3(x.b), v = p3(x.c);
+    P3 n = crossp(u, v);
+    double len = std::sqrt(dotp(n, n));
+    P3 nn = (len > 1e-8) ? P3{n.x * (1.0 / len), n.y * (1.0 / len), n.z * (1.0 / len)}
+                         : P3{1.0, 0.0, 0.0};
+    P3 w = scl(1 / dotp(n, n), n);
+    double Qa[3] = {Q.x, Q.y, Q.z}, ua[3] = {u.x, u.y, u.z}, va[3] = {v.x, v.y, v.z};
+    double na[3] = {nn.x, nn.y, nn.z}, wa[3] = {w.x, w.y, w.z};
+    for (int i = 0; i < 3; ++i) {
+      q.Q[i] = Qa[i];
+      q.u[i] = ua[i];
+      q.v[i] = va[i];
+      q.n[i] = na[i];
+      q.w[i] = wa[i];
+    }
+    q.D = dotp(nn, Q);
+    q.area = len;
+    quad_of[o] = (int)H.quads.size();
+    H.quads.push_back(q);
+    return quad_of[o];
+  }
+
+  int emit_chain(const std::vector<int> &chain) {
+    int first = (int)H.xforms.size();
+    for (int o : chain) {
+      const rt_object_desc &x = D->objects[o];
+      DXform X;
+      std::memset(&X, 0, sizeof X);
+      if (x.kind == RT_OBJ_TRANSLATE) {
+        X.kind = X_TRANSLATE;
+        X.a = x.a.x;
+        X.b = x.a.y;
+        X.c = x.a.z;
+      } else { // RotateY.cpp:7-9
+        double rad = x.s * kPi / 180.0;
+        X.kind = X_ROTATE_Y;
+        X.a = std::sin(rad);
+        X.b = std::cos(rad);
+      }
+      H.xforms.push_back(X);
+    }
+    return first;
+  }
+
+  // Reference box rules for RotateY (RotateY.cpp:10-34) and Translate
+  // (AABBUtility.hpp:7-11), applied innermost transform first.
+  Bx rot_box(const Bx &cb, double angle) {
+    double rad = angle * kPi / 180.0;
+    double s = std::sin(rad), c = std::cos(rad);
+    double mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 2; k++) {
+          double px = i * cb.hi[0] + (1 - i) * cb.lo[0];
+          double py = j * cb.hi[1] + (1 - j) * cb.lo[1];
+          double pz = k * cb.hi[2] + (1 - k) * cb.lo[2];
+          double t[3] = {c * px + s * pz, py, -s * px + c * pz};
+          for (int a = 0; a < 3; a++) {
+            mn[a] = std::fmin(mn[a], t[a]);
+            mx[a] = std::fmax(mx[a], t[a]);
+          }
+        }
+    return bx_points(P3{mn[0], mn[1], mn[2]}, P3{mx[0], mx[1], mx[2]});
+  }
+  Bx trans_box(const Bx &cb, const rt_vec3 &off) {
+    Bx b;
+    double o[3] = {off.x, off.y, off.z};
+    for (int i = 0; i < 3; ++i) {
+      b.lo[i] = cb.lo[i] + o[i];
+      b.hi[i] = cb.hi[i] + o[i];
+    }
+    bx_pad(b);
+    return b;
+  }
+  Bx chain_box(Bx b, const std::vector<int> &chain) {
+    for (size_t k = chain.size(); k-- > 0;) {
+      const rt_object_desc &x = D->objects[chain[k]];
+      b = (x.kind == RT_OBJ_ROTATE_Y) ? rot_box(b, x.s) : trans_box(b, x.a);
+    }
+    return b;
+  }
+
+  bool make_item(const FItem &f, DItem &it, Bx &bb) {
+    std::memset(&it, 0, sizeof it);
+    const rt_object_desc &x = D->objects[f.obj];
+    it.kind = f.kind;
+    it.id = f.obj;
+    it.mat = -1;
+    if (f.kind == I_SPHERE || f.kind == I_QUAD) {
+      it.idx = (f.kind == I_SPHERE) ? sphere_record(f.obj) : quad_record(f.obj);
+      it.mat = x.material;
+      bb = chain_box(box[f.obj], f.chain);
+    } else { // medium: boundary items in the medium's local frame
+      std::vector<FItem> bs;
+      std::vector<int> ch0;
+      if (!flatten(x.child, ch0, bs, true)) return false;
+      DMedium m;
+      std::memset(&m, 0, sizeof m);
+      m.neg_inv_density = -1.0 / x.s; // ConstantMedium.cpp:73
+      m.phase = x.phase;
+      m.id = f.obj;
+      Bx ub = bx_empty();
+      std::vector<DItem> tmp;
+      for (const FItem &b : bs) {
+        DItem bi;
+        Bx b1;
+        if (!make_item(b, bi, b1)) return false;
+        tmp.push_back(bi);
+        ub = bx_join(ub, b1);
+      }
+      m.b_first = (int32_t)H.bitems.size();
+      m.b_count = (int32_t)tmp.size();
+      for (auto &bi : tmp) H.bitems.push_back(bi);
+      it.idx = (int32_t)H.media.size();
+      H.media.push_back(m);
+      bb = chain_box(ub, f.chain);
+    }
+    it.xf_first = emit_chain(f.chain);
+    it.xf_count = (int32_t)f.chain.size();
+    return true;
+  }
+
+  void emit_materials() {
+    for (int i = 0; i < D->n_materials; ++i) {
+      const rt_material_desc &m = D->materials[i];
+      DMat d;
+      std::memset(&d, 0, sizeof d);
+      d.kind = m.kind;
+      d.tex = m.texture;
+      d.albedo[0] = m.albedo.x, d.albedo[1] = m.albedo.y, d.albedo[2] = m.albedo.z;
+      d.fuzz = m.fuzz;
+      d.ior = m.refraction_index;
+      H.mats.push_back(d);
+    }
+    for (int i = 0; i < D->n_textures; ++i) {
+      const rt_texture_desc &t = D->textures[i];
+      DTex d;
+      std::memset(&d, 0, sizeof d);
+      d.kind = t.kind;
+      d.even = t.even;
+      d.odd = t.odd;
+      d.perlin = t.perlin;
+      d.scale = t.scale;
+      d.color[0] = t.color.x, d.color[1] = t.color.y, d.color[2] = t.color.z;
+      H.texs.push_back(d);
+    }
+    for (int i = 0; i < D->n_perlin; ++i) {
+      DPerlin p;
+      for (int k = 0; k < 256; ++k) {
+        p.rv[k][0] = D->perlin[i].rand_vec[k].x;
+        p.rv[k][1] = D->perlin[i].rand_vec[k].y;
+        p.rv[k][2] = D->perlin[i].rand_vec[k].z;
+        p.px[k] = D->perlin[i].perm_x[k] & 255;
+        p.py[k] = D->perlin[i].perm_y[k] & 255;
+        p.pz[k] = D->perlin[i].perm_z[k] & 255;
+      }
+      H.perlin.push_back(p);
+    }
+  }
+
+  // ---------------------------------------------------------------- world BVH
+  struct BRef {
+    Bx b;
+    P3 c;
+    int32_t obj;
+  };
+  struct BNode {
+    Bx b;
+    int left = -1, right = -1; // build-node indices, -1 for leaves
+    int first = 0, count = 0;  // leaf ref range
+  };
+  std::vector<BNode> bn;
+  int max_depth_seen = 0;
+
+  int build(std::vector<BRef> &r, int st, int en, int dep) {
+    BNode n;
+    n.b = bx_empty();
+    Bx cb = bx_empty();
+    for (int i = st; i < en; ++i) {
+      n.b = bx_join(n.b, r[i].b);
+      Bx pc{{r[i].c.x, r[i].c.y, r[i].c.z}, {r[i].c.x, r[i].c.y, r[i].c.z}};
+      cb = bx_join(cb, pc);
+    }
+    int cnt = en - st;
+    max_depth_seen = std::max(max_depth_seen, dep);
+    int id = (int)bn.size();
+    bn.push_back(n);
+    const int kLeafMax = 2;
+    if (cnt <= kLeafMax) {
+      bn[id].first = st;
+      bn[id].count = cnt;
+      return id;
+    }
+    // depth budget: switch to balanced median splits when the SAH tree risks
+    // exceeding the per-lane traversal stack (RT_STACK_DEPTH)
+    int need = 0;
+    while ((1 << need) < cnt) ++need;
+    bool force_median = dep + need >= RT_STACK_DEPTH - 2;
+    int best_axis = -1, best_bin = -1;
+    double best_cost = kInf;
+    const int kBins = 16;
+    if (!force_median) {
+      for (int ax = 0; ax < 3; ++ax) {
+        double lo = cb.lo[ax], hi = cb.hi[ax];
+        if (!(hi - lo > 1e-12)) continue;
+        Bx bb[kBins];
+        int bc[kBins];
+        for (int k = 0; k < kBins; ++k) {
+          bb[k] = bx_empty();
+          bc[k] = 0;
+        }
+        double sc = kBins / (hi - lo);
+        for (int i = st; i < en; ++i) {
+          int k = std::min(kBins - 1, std::max(0, (int)((comp(r[i].c, ax) - lo) * sc)));
+          bb[k] = bx_join(bb[k], r[i].b);
+          bc[k]++;
+        }
+        Bx lb[kBins];
+        int lc[kBins];
+        Bx acc = bx_empty();
+        int a = 0;
+        for (int k = 0; k < kBins; ++k) {
+          acc = bx_join(acc, bb[k]);
+          a += bc[k];
+          lb[k] = acc;
+          lc[k] = a;
+        }
+        acc = bx_empty();
+        a = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          acc = bx_join(acc, bb[k]);
+          a += bc[k];
+          int nl = lc[k - 1], nr = a;
+          if (nl == 0 || nr == 0) continue;
+          double cost = bx_area(lb[k - 1]) * nl + bx_area(acc) * nr;
+          if (cost < best_cost) {
+            best_cost = cost;
+            best_axis = ax;
+            best_bin = k;
+          }
+        }
+      }
+    }
+    int mid;
+    if (best_axis >= 0) {
+      double lo = cb.lo[best_axis], hi = cb.hi[best_axis];
+      double sc = kBins / (hi - lo);
+      auto it = std::partition(r.begin() + st, r.begin() + en, [&](const BRef &x) {
+        int k = std::min(kBins - 1, std::max(0, (int)((comp(x.c, best_axis) - lo) * sc)));
+        return k < best_bin;
+      });
+      mid = int(it - r.begin());
+      // leaf if splitting does not pay (SAH with traversal cost 1, isect cost 1)
+      double parent_area = bx_area(bn[id].b);
+      if (cnt <= 4 && parent_area > 0 && 1.0 + best_cost / parent_area >= (double)cnt) {
+        bn[id].first = st;
+        bn[id].count = cnt;
+        return id;
+      }
+    } else {
+      mid = st + cnt / 2;
+    }
+    if (mid <= st || mid >= en) {
+      int ax = bx_longest(cb);
+      std::sort(r.begin() + st, r.begin() + en,
+                [ax](const BRef &a, const BRef &b) { return comp(a.c, ax) < comp(b.c, ax); });
+      mid = st + cnt / 2;
+    }
+    int L = build(r, st, mid, dep + 1);
+    int R = build(r, mid, en, dep + 1);
+    bn[id].left = L;
+    bn[id].right = R;
+    return id;
+  }
+
+  void emit_world_bvh(const std::vector<Bx> &item_box) {
+    std::vector<BRef> r;
+    for (size_t i = 0; i < item_box.size(); ++i) {
+      BRef x;
+      x.b = item_box[i];
+      x.c = bx_center(x.b);
+      x.obj = (int32_t)i;
+      r.push_back(x);
+    }
+    if (r.empty()) {
+      H.root_is_leaf = 1;
+      H.n_root_refs = 0;
+      return;
+    }
+    bn.clear();
+    int root = build(r, 0, (int)r.size(), 0);
+    H.bvh_depth = max_depth_seen;
+    for (auto &x : r) H.refs.push_back(x.obj);
+    if (bn[root].left < 0) {
+      H.root_is_leaf = 1;
+      H.n_root_refs = bn[root].count;
+      return;
+    }
+    // flatten: DFS over inner build nodes; each DNode holds both children's boxes
+    std::vector<int> map(bn.size(), -1);
+    std::vector<int> order;
+    std::function<void(int)> dfs = [&](int b) {
+      if (bn[b].left < 0) return;
+      map[b] = (int)order.size();
+      order.push_back(b);
+      dfs(bn[b].left);
+      dfs(bn[b].right);
+    };
+    dfs(root);
+    H.nodes.resize(order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+      const BNode &p = bn[order[i]];
+      DNode &d = H.nodes[i];
+      std::memset(&d, 0, sizeof d);
+      int ch[2] = {p.left, p.right};
+      for (int k = 0; k < 2; ++k) {
+        const BNode &c = bn[ch[k]];
+        for (int a = 0; a < 3; ++a) {
+          d.lo[k][a] = c.b.lo[a];
+          d.hi[k][a] = c.b.hi[a];
+        }
+        if (c.left < 0) {
+          d.child[k] = ~c.first;
+          d.count[k] = c.count;
+        } else {
+          d.child[k] = map[ch[k]];
+          d.count[k] = 0;
+        }
+      }
+    }
+  }
+
+  // ------------------------------------------------------------ light leaves
+  // BVHNode's split of a light list (BVHNode.cpp:21-123); returns a nested
+  // description as a vector of (object, weight) pairs in DFS order.
+  void ref_bvh_leaves(std::vector<int32_t> objs, size_t st, size_t en, double w,
+                      std::vector<std::pair<int32_t, double>> &out) {
+    size_t span = en - st;
+    if (span <= 4) {
+      if (span == 1) {
+        out.push_back({objs[st], w * 0.5});
+        out.push_back({objs[st], w * 0.5});
+      } else if (span == 2) {
+        out.push_back({objs[st], w * 0.5});
+        out.push_back({objs[st + 1], w * 0.5});
+      } else {
+        size_t mid = st + span / 2;
+        ref_bvh_leaves(objs, st, mid, w * 0.5, out);
+        ref_bvh_leaves(objs, mid, en, w * 0.5, out);
+      }
+      return;
+    }
+    // general case: SAH over 15 candidate planes per axis, std::partition
+    Bx me = bx_empty(), cb = bx_empty();
+    for (size_t i = st; i < en; ++i) {
+      me = bx_join(me, box[objs[i]]);
+      P3 c = bx_center(box[objs[i]]);
+      cb = bx_join(cb, bx_points(c, c));
+    }
+    auto cost_of = [&](int ax, double pos, size_t &lc, size_t &rc) {
+      Bx lb = bx_empty(), rb = bx_empty();
+      lc = rc = 0;
+      for (size_t i = st; i < en; ++i) {
+        const Bx &b = box[objs[i]];
+        if (comp(bx_center(b), ax) < pos) {
+          lb = bx_join(lb, b);
+          ++lc;
+        } else {
+          rb = bx_join(rb, b);
+          ++rc;
+        }
+      }
+      if (lc == 0 || rc == 0) return kInf;
+      double tot = bx_area(me);
+      if (tot < 1e-9) return kInf;
+      return 1.0 + (bx_area(lb) / tot) * lc * 2.0 + (bx_area(rb) / tot) * rc * 2.0;
+    };
+    int bax = 0;
+    double bpos = 0, bcost = kInf;
+    size_t bl = 0, br = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+      double amin = cb.lo[ax], amax = cb.hi[ax];
+      if (amax - amin < 1e-9) continue;
+      for (int i = 1; i < 16; ++i) {
+        double pos = amin + (static_cast<double>(i) / 16) * (amax - amin);
+        size_t lc, rc;
+        double c = cost_of(ax, pos, lc, rc);
+        if (c < bcost) {
+          bcost = c;
+          bax = ax;
+          bpos = pos;
+          bl = lc;
+          br = rc;
+        }
+      }
+    }
+    size_t mid;
+    if (bcost == kInf || bl == 0 || br == 0) {
+      int ax = bx_longest(me);
+      std::sort(objs.begin() + st, objs.begin() + en,
+                [&](int32_t a, int32_t b) { return box[a].lo[ax] < box[b].lo[ax]; });
+      mid = st + span / 2;
+    } else {
+      auto it = std::partition(objs.begin() + st, objs.begin() + en, [&](int32_t o) {
+        return comp(bx_center(box[o]), bax) < bpos;
+      });
+      mid = size_t(it - objs.begin());
+      if (mid == st || mid == en) mid = st + span / 2;
+    }
+    ref_bvh_leaves(objs, st, mid, w * 0.5, out);
+    ref_bvh_leaves(objs, mid, en, w * 0.5, out);
+  }
+
+  bool add_light(int32_t o, double w, std::vector<int32_t> &chain) {
+    const rt_object_desc &x = D->objects[o];
+    if (x.kind == RT_OBJ_LIST) { // HittableList::pdf_value / random, HittableList.cpp:44-63
+      double cw = w * (1.0 / x.count);
+      for (int k = 0; k < x.count; ++k)
+        if (!add_light(D->children[x.child + k], cw, chain)) return false;
+      return true;
+    }
+    if (x.kind == RT_OBJ_ROTATE_Y || x.kind == RT_OBJ_TRANSLATE) {
+      if ((int)chain.size() >= RT_MAX_CHAIN)
+        return fail("UNSUPPORTED: light transform chain deeper than RT_MAX_CHAIN");
+      chain.push_back(o);
+      bool ok = add_light(x.child, w, chain);
+      chain.pop_back();
+      return ok;
+    }
+    DLight L;
+    std::memset(&L, 0, sizeof L);
+    if (x.kind == RT_OBJ_SPHERE) {
+      L.kind = I_SPHERE;
+      L.idx = sphere_record(o);
+    } else if (x.kind == RT_OBJ_QUAD) {
+      L.kind = I_QUAD;
+      L.idx = quad_record(o);
+    } else {
+      L.kind = I_NONE; // Hittable defaults: pdf 0, random (1,0,0)
+    }
+    std::vector<int> ch(chain.begin(), chain.end());
+    L.xf_first = emit_chain(ch);
+    L.xf_count = (int32_t)chain.size();
+    L.weight = w;
+    H.lights.push_back(L);
+    return true;
+  }
+
+  bool emit_lights() {
+    if (D->lights < 0) return true;
+    const rt_object_desc &lx = D->objects[D->lights];
+    if (lx.count == 0) return true;
+    std::vector<int32_t> chain;
+    if (D->use_bvh) {
+      std::vector<int32_t> objs(D->children + lx.child, D->children + lx.child + lx.count);
+      std::vector<std::pair<int32_t, double>> leaves;
+      ref_bvh_leaves(objs, 0, objs.size(), 1.0, leaves);
+      for (auto &p : leaves)
+        if (!add_light(p.first, p.second, chain)) return false;
+    } else {
+      if (!add_light(D->lights, 1.0, chain)) return false;
+    }
+    double c = 0;
+    for (auto &L : H.lights) {
+      c += L.weight;
+      L.cum = c;
+    }
+    return true;
+  }
+
+  bool run() {
+    if (!D) return fail("null scene description");
+    if (D->n_objects <= 0 || !D->objects) return fail("scene has no objects");
+    if (D->n_textures < 0 || D->n_materials < 0 || D->n_perlin < 0 || D->n_children < 0)
+      return fail("negative table size");
+    if ((D->n_textures && !D->textures) || (D->n_materials && !D->materials) ||
+        (D->n_perlin && !D->perlin) || (D->n_children && !D->children))
+      return fail("null table pointer");
+    box.assign(D->n_objects, bx_empty());
+    state.assign(D->n_objects, 0);
+    depth.assign(D->n_objects, 0);
+    sphere_of.assign(D->n_objects, -1);
+    quad_of.assign(D->n_objects, -1);
+    if (D->world < 0 || D->world >= D->n_objects || D->objects[D->world].kind != RT_OBJ_LIST)
+      return fail("world must be a list object");
+    if (D->lights >= D->n_objects ||
+        (D->lights >= 0 && D->objects[D->lights].kind != RT_OBJ_LIST))
+      return fail("lights must be a list object or -1");
+    for (int o = 0; o < D->n_objects; ++o)
+      if (!visit(o)) return false;
+    if (!check_world_materials(D->world)) return false;
+    std::vector<FItem> fitems;
+    std::vector<int> chain;
+    if (!flatten(D->world, chain, fitems, false)) return false;
+    std::vector<Bx> ibox;
+    for (const FItem &f : fitems) {
+      DItem it;
+      Bx bb;
+      if (!make_item(f, it, bb)) return false;
+      H.items.push_back(it);
+      ibox.push_back(bb);
+    }
+    emit_materials();
+    emit_world_bvh(ibox);
+    return emit_lights();
+  }
+};
+
+} // namespace
+
+int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err) {
+  Compiler c(desc, out, err);
+  if (!c.run()) return err.rfind("UNSUPPORTED", 0) == 0 ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID;
+  return RT_OK;
+}
+
+int camera_setup(const rt_camera_desc *cd, rt_frame *f, std::string &err) {
+  if (!cd || !f) {
+    err = "null camera";
+    return RT_ERR_INVALID;
+  }
+  if (cd->image_width < 1 || cd->samples_per_pixel < 1 || cd->max_depth < 0 ||
+      !(cd->aspect_ratio > 0)) {
+    err = "invalid camera (image_width/samples_per_pixel >= 1, aspect_ratio > 0)";
+    return RT_ERR_INVALID;
+  }
+  // Camera::initialize, Camera.cpp:31-73
+  int W = cd->image_width;
+  int H = int(W / cd->aspect_ratio);
+  H = (H < 1) ? 1 : H;
+  double theta = cd->vfov * kPi / 180.0;
+  double h = std::tan(theta / 2);
+  double vh = 2 * h * cd->focus_dist;
+  double vw = vh * (double(W) / H);
+  auto unit = [](P3 v) {
+    double l = std::sqrt(dotp(v, v));
+    if (l > 1e-8) {
+      double s = 1.0 / l;
+      return P3{v.x * s, v.y * s, v.z * s};
+    }
+    return P3{1.0, 0.0, 0.0};
+  };
+  P3 from = p3(cd->lookfrom), at = p3(cd->lookat), up = p3(cd->vup);
+  P3 w = unit(sub(from, at));
+  P3 u = unit(crossp(up, w));
+  P3 v = crossp(w, u);
+  P3 vu = scl(vw, u);
+  P3 vv = scl(vh, P3{-v.x, -v.y, -v.z});
+  P3 du = scl(1 / double(W), vu);
+  P3 dv = scl(1 / double(H), vv);
+  P3 ul = sub(sub(sub(from, scl(cd->focus_dist, w)), scl(1 / 2.0, vu)), scl(1 / 2.0, vv));
+  P3 p00 = add(ul, scl(0.5, add(du, dv)));
+  double rad = cd->focus_dist * std::tan((cd->defocus_angle / 2) * kPi / 180.0);
+  auto rv = [](P3 a) { return rt_vec3{a.x, a.y, a.z}; };
+  f->image_width = W;
+  f->image_height = H;
+  f->sqrt_spp = int(std::sqrt(cd->samples_per_pixel));
+  f->max_depth = cd->max_depth;
+  f->center = rv(from);
+  f->pixel00_loc = rv(p00);
+  f->pixel_delta_u = rv(du);
+  f->pixel_delta_v = rv(dv);
+  f->u = rv(u);
+  f->v = rv(v);
+  f->w = rv(w);
+  f->defocus_disk_u = rv(scl(rad, u));
+  f->defocus_disk_v = rv(scl(rad, v));
+  f->defocus_angle = cd->defocus_angle;
+  f->pixel_samples_scale = 1.0 / cd->samples_per_pixel;
+  f->background = cd->background;
+  return RT_OK;
+}
+
+} // namespace rtx

@@ -1,0 +1,106 @@
+"""Host-side mirror of the reference's StaticCamera for the HIP path.
+
+    StaticCamera(config, out).render(world, lights)   (StaticCamera.cpp:25-30)
+ -> Renderer(scene).render(camera) / render_ppm(...)
+
+Camera setup, scene upload, the render launch and the PPM writer are the
+reference's steps; the per-pixel work runs in the HIP kernel behind the C ABI.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .lib import check, load
+from .ppm import write_ppm
+
+
+def camera_frame(cam):
+    """Camera::initialize (Camera.cpp:31-73) via rt_camera_setup."""
+    f = abi.Frame()
+    check(load().rt_camera_setup(C.byref(cam), C.byref(f)))
+    return f
+
+
+class Renderer:
+    """Owns one device-side scene (rt_scene) on one GPU."""
+
+    def __init__(self, scene, device=0):
+        self.lib = load()
+        self.scene_desc = scene
+        self._desc = scene.desc()
+        h = C.c_void_p()
+        check(self.lib.rt_scene_create(C.byref(self._desc), int(device), C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.rt_scene_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        i = abi.SceneInfo()
+        check(self.lib.rt_scene_info_get(self.handle, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in abi.SceneInfo._fields_}
+
+    @staticmethod
+    def params(seed=0, rows=(0, 0), samples=(0, -1), output=abi.RT_OUT_SCALED, accumulate=0):
+        p = abi.RenderParams()
+        p.row_begin, p.row_end = int(rows[0]), int(rows[1])
+        p.sample_begin, p.sample_count = int(samples[0]), int(samples[1])
+        p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        p.output = int(output)
+        p.accumulate = int(accumulate)
+        return p
+
+    def render(self, frame, seed=0, rows=(0, 0), samples=(0, -1), output=abi.RT_OUT_SCALED):
+        """Synchronous render -> float64 array [rows, W, 3] (host)."""
+        r0, r1 = rows
+        if r0 == 0 and r1 == 0:  # the ABI's "whole image"
+            r1 = frame.image_height
+        out = np.empty((max(0, r1 - r0), frame.image_width, 3), dtype=np.float64)
+        p = self.params(seed, (r0, r1), samples, output)
+        check(self.lib.rt_render(self.handle, C.byref(frame), C.byref(p),
+                                 out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def render_device(self, frame, dev_ptr, stream_ptr=None, seed=0, rows=(0, 0), samples=(0, -1),
+                      output=abi.RT_OUT_SUM, accumulate=1):
+        """Asynchronous render into a device buffer (e.g. a torch.cuda tensor's data_ptr())."""
+        p = self.params(seed, rows, samples, output, accumulate)
+        check(self.lib.rt_render_device(self.handle, C.byref(frame), C.byref(p),
+                                        C.c_void_p(dev_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def stats(self, frame, seed=0, rows=(0, 0), samples=(0, -1)):
+        s = abi.PathStats()
+        p = self.params(seed, rows, samples)
+        check(self.lib.rt_render_stats(self.handle, C.byref(frame), C.byref(p), C.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.PathStats._fields_}
+
+    def last_kernel_ms(self):
+        ms = C.c_double()
+        check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))
+        return ms.value
+
+
+def render_ppm(scene, path, device=0, seed=0, **cam_overrides):
+    """StaticCamera::render on the HIP path: camera setup, render, PPM."""
+    cam = scene.camera_desc(**cam_overrides)
+    frame = camera_frame(cam)
+    with Renderer(scene, device) as R:
+        img = R.render(frame, seed=seed)
+    write_ppm(path, img)
+    return img

@@ -110,3 +110,17 @@ def ref_render(scene, cam, seed, use_bvh=None):
     bvh = scene.use_bvh if use_bvh is None else use_bvh
     ref().ref_render(C.byref(d), C.byref(cam), seed, int(bvh), dptr(out))
     return out
+
+
+def ref_trace_parallel(scene, cam, threads, use_bvh=None):
+    """Reference code, -p decomposition over `threads` host threads (CPU baseline)."""
+    d = scene.desc()
+    h = image_height(cam)
+    out = np.zeros((h, cam.image_width, 3), dtype=np.float64)
+    bvh = scene.use_bvh if use_bvh is None else use_bvh
+    L = ref()
+    L.ref_trace_parallel.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.CameraDesc), C.c_int,
+                                     C.c_int, C.POINTER(C.c_double)]
+    L.ref_trace_parallel.restype = C.c_longlong
+    n = L.ref_trace_parallel(C.byref(d), C.byref(cam), int(bvh), int(threads), dptr(out))
+    return n, out
