@@ -135,9 +135,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step(seed):
-        acc.zero_()
+        # each rank overwrites its partial sums (no memset, no read-modify-write)
         R.render_device(frame, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=(s0, s1 - s0),
-                        output=abi.RT_OUT_SUM, accumulate=1)
+                        output=abi.RT_OUT_SUM, accumulate=0)
         if ws > 1:
             dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
 

@@ -215,6 +215,8 @@ typedef struct rt_scene_info {
   int32_t sphere_bytes; /* bytes per sphere record */
   int32_t quad_bytes;   /* bytes per quad record */
   int64_t device_bytes; /* total device bytes of the scene */
+  int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise */
+  int32_t _pad;
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -227,6 +228,19 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   d.n_nodes = (int32_t)H.nodes.size();
   d.root_is_leaf = H.root_is_leaf;
   d.n_root_refs = H.n_root_refs;
+  d.features = 0;
+  for (const DItem &it : H.items) {
+    if (it.kind == I_MEDIUM) d.features |= RT_FEAT_MEDIA;
+    if (it.xf_count) d.features |= RT_FEAT_XFORM;
+  }
+  for (const DLight &L : H.lights)
+    if (L.xf_count) d.features |= RT_FEAT_XFORM;
+  if (!H.lights.empty()) d.features |= RT_FEAT_LIGHTS;
+  for (const DTex &t : H.texs)
+    if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
+  if (const char *fx = std::getenv("RTX_EXTRA_FEATURES")) // debug: widen the instance
+    d.features |= std::atoi(fx) & 15;
+  d.pad = 0;
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
 
   rt_scene_info &in = s->info;
@@ -242,6 +256,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.sphere_bytes = (int32_t)sizeof(DSphere);
   in.quad_bytes = (int32_t)sizeof(DQuad);
   in.device_bytes = (int64_t)off;
+  in.features = d.features;
   *out = s;
   return RT_OK;
 }

@@ -14,622 +14,28 @@
 //  * stateless Philox4x32-10 random numbers keyed by (seed; pixel, stratum,
 //    bounce, slot) — no per-pixel curandState traffic (48 B/pixel/sample in the
 //    reference) and sample ranges shard across GPUs exactly;
-//  * BVH traversal with both child boxes per node and a per-lane stack in LDS
-//    (stack[depth][lane]: consecutive lanes hit consecutive banks);
+//  * BVH traversal (rt_path.h) with both child boxes per node, near-first
+//    while-while order and a per-lane stack in LDS (stack[depth][lane]:
+//    consecutive lanes on consecutive banks);
 //  * per-pixel fp64 sums in LDS (ds_add_f64), written once per tile with
-//    coalesced stores.
+//    coalesced stores;
+//  * scene-feature specialisation: the launcher picks the instance compiled for
+//    the features the scene uses (media, transform chains, light sampling,
+//    Perlin noise), so e.g. a sphere-only scene runs without the fog and
+//    light-sampling code and its register cost.
 // All arithmetic is fp64 like the reference (Vec3.hpp:184); built with
 // -ffp-contract=off so expression rounding follows the reference's order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/rt_api.h"
-#include "rt_layout.h"
+#include "rt_path.h"
 
 namespace {
 
-constexpr double kInf = __builtin_huge_val();
-constexpr double kPi = 3.1415926535897932385;
-constexpr uint32_t kCamTag = 0xFFFFFFFFu;
-constexpr uint32_t kSlotEvent = 0, kSlotDir = 1, kSlotMediumBase = 0x100;
+using namespace rtp;
 constexpr int kWaves = 4; // waves (tiles) per 256-thread block
 
-struct V3 {
-  double x, y, z;
-};
-__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 ld3(const double *p) { return V3{p[0], p[1], p[2]}; }
-__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ V3 operator*(double t, V3 a) { return v3(t * a.x, t * a.y, t * a.z); }
-__device__ __forceinline__ V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
-  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ V3 unitv(V3 a) { // Vec3::normalize (Vec3.hpp:150-158)
-  double l = sqrt(len2(a));
-  if (l > 1e-8) {
-    double s = 1.0 / l;
-    return v3(a.x * s, a.y * s, a.z * s);
-  }
-  return v3(1.0, 0.0, 0.0);
-}
-__device__ __forceinline__ double comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
-
-struct Ray {
-  V3 o, d;
-  double tm;
-};
-__device__ __forceinline__ V3 at(const Ray &r, double t) {
-  return v3(r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z);
-}
-
-struct Hit {
-  double t;
-  V3 p, n;
-  int mat;
-  bool front;
-};
-
-// ---------------------------------------------------------------- RNG
-struct Key {
-  uint32_t k0, k1, pixel, sample;
-};
-__device__ __forceinline__ void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                         uint32_t k0, uint32_t k1, uint32_t out[4]) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0;
-    c1 = lo1;
-    c2 = n2;
-    c3 = lo0;
-  }
-  out[0] = c0;
-  out[1] = c1;
-  out[2] = c2;
-  out[3] = c3;
-}
-// Two 53-bit uniforms in [0,1) for (bounce, slot) — DESIGN.md "RNG contract".
-__device__ __forceinline__ void u01x2(const Key &k, uint32_t bounce, uint32_t slot, double &a,
-                                      double &b) {
-  uint32_t x[4];
-  philox10(k.pixel, k.sample, bounce, slot, k.k0, k.k1, x);
-  uint64_t ua = ((uint64_t)x[0] << 32) | x[1];
-  uint64_t ub = ((uint64_t)x[2] << 32) | x[3];
-  a = (double)(ua >> 11) * 0x1.0p-53;
-  b = (double)(ub >> 11) * 0x1.0p-53;
-}
-
-// ---------------------------------------------------------------- textures
-__device__ double perlin_noise(const DPerlin &P, V3 p) { // PerlinNoise.hpp:43-60, 186-201
-  double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
-  double u = p.x - fx, v = p.y - fy, w = p.z - fz;
-  int xi = (int)fx, yi = (int)fy, zi = (int)fz;
-  double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
-  double acc = 0.0;
-  for (int i = 0; i < 2; i++) {
-    int pxi = P.px[(xi + i) & 255];
-    double fi = i * uu + (1 - i) * (1 - uu);
-    for (int j = 0; j < 2; j++) {
-      int pyj = P.py[(yi + j) & 255];
-      double fj = j * vv + (1 - j) * (1 - vv);
-      for (int k = 0; k < 2; k++) {
-        const double *g = P.rv[pxi ^ pyj ^ P.pz[(zi + k) & 255]];
-        V3 wv = v3(u - i, v - j, w - k);
-        acc += fi * fj * (k * ww + (1 - k) * (1 - ww)) * dot(ld3(g), wv);
-      }
-    }
-  }
-  return acc;
-}
-
-__device__ V3 tex_value(const DScene &S, int t, V3 p) {
-  for (int guard = 0; guard < 64; ++guard) {
-    const DTex &T = S.texs[t];
-    if (T.kind == RT_TEX_SOLID) return ld3(T.color);
-    if (T.kind == RT_TEX_CHECKER) { // CheckerTexture.cpp:41-55
-      double inv = 1.0 / T.scale;
-      int xi = (int)floor(inv * p.x), yi = (int)floor(inv * p.y), zi = (int)floor(inv * p.z);
-      t = ((xi + yi + zi) % 2 == 0) ? T.even : T.odd;
-      continue;
-    }
-    // NoiseTexture.cpp:31-34: 0.5 * (1 + sin(scale*z + 10*turb(p, 7)))
-    const DPerlin &P = S.perlin[T.perlin];
-    double acc = 0.0, wgt = 1.0;
-    V3 q = p;
-    for (int i = 0; i < 7; i++) {
-      acc += wgt * perlin_noise(P, q);
-      wgt *= 0.5;
-      q = v3(q.x * 2, q.y * 2, q.z * 2);
-    }
-    double f = 1 + sin(T.scale * p.z + 10 * fabs(acc));
-    return f * v3(0.5, 0.5, 0.5);
-  }
-  return v3(0, 0, 0);
-}
-
-// ------------------------------------------------------------ primitives
-// Sphere::hit root search (Sphere.cpp:101-127); returns the root or -1 sentinel.
-__device__ __forceinline__ bool sphere_root(const DSphere &s, const Ray &r, double a, double tmin,
-                                            double tmax, double &root, V3 &cc) {
-  cc = v3(s.c0[0] + r.tm * s.dir[0], s.c0[1] + r.tm * s.dir[1], s.c0[2] + r.tm * s.dir[2]);
-  V3 oc = cc - r.o;
-  double h = dot(r.d, oc);
-  double c = len2(oc) - s.rr;
-  double disc = h * h - a * c;
-  if (disc < 0) return false;
-  double sq = sqrt(disc);
-  double t = (h - sq) / a;
-  if (!(tmin < t && t < tmax)) {
-    t = (h + sq) / a;
-    if (!(tmin < t && t < tmax)) return false;
-  }
-  root = t;
-  return true;
-}
-__device__ __forceinline__ void sphere_record(const DSphere &s, const Ray &r, double t, V3 cc,
-                                              int mat, Hit &h) {
-  h.t = t;
-  h.p = at(r, t);
-  V3 on = (1 / s.r) * (h.p - cc);
-  h.front = dot(r.d, on) < 0;
-  h.n = h.front ? on : -on;
-  h.mat = mat;
-  // u,v (Sphere.cpp:136-140) are not computed: no texture kind reads them.
-}
-
-__device__ __forceinline__ bool quad_t(const DQuad &q, const Ray &r, double tmin, double tmax,
-                                       double &t) { // Plane.cpp:76-100
-  V3 n = ld3(q.n);
-  double denom = dot(n, r.d);
-  if (fabs(denom) < 1e-8) return false;
-  double tt = (q.D - dot(n, r.o)) / denom;
-  if (!(tmin <= tt && tt <= tmax)) return false;
-  V3 pv = at(r, tt) - ld3(q.Q);
-  V3 w = ld3(q.w);
-  double alpha = dot(w, cross(pv, ld3(q.v)));
-  double beta = dot(w, cross(ld3(q.u), pv));
-  if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) return false;
-  t = tt;
-  return true;
-}
-__device__ __forceinline__ void quad_record(const DQuad &q, const Ray &r, double t, int mat,
-                                            Hit &h) {
-  h.t = t;
-  h.p = at(r, t);
-  V3 n = ld3(q.n);
-  h.front = dot(r.d, n) < 0;
-  h.n = h.front ? n : -n;
-  h.mat = mat;
-}
-
-// ------------------------------------------------------ transform chains
-// RotateY (RotateY.cpp:41-76) / Translate (Translate.cpp:17-31) as flattened
-// chains: world -> local applies ops outermost first, the record goes back
-// innermost first.
-__device__ __forceinline__ V3 rot_in(double s, double c, V3 p) {
-  return v3((c * p.x) - (s * p.z), p.y, (s * p.x) + (c * p.z));
-}
-__device__ __forceinline__ V3 rot_out(double s, double c, V3 p) {
-  return v3((c * p.x) + (s * p.z), p.y, (-s * p.x) + (c * p.z));
-}
-__device__ __forceinline__ Ray to_local(const DScene &S, int f, int n, Ray r) {
-  for (int k = 0; k < n; ++k) {
-    const DXform X = S.xforms[f + k];
-    if (X.kind == X_TRANSLATE) {
-      r.o = r.o - v3(X.a, X.b, X.c);
-    } else {
-      r.o = rot_in(X.a, X.b, r.o);
-      r.d = rot_in(X.a, X.b, r.d);
-    }
-  }
-  return r;
-}
-__device__ __forceinline__ void to_world(const DScene &S, int f, int n, Hit &h) {
-  for (int k = n - 1; k >= 0; --k) {
-    const DXform X = S.xforms[f + k];
-    if (X.kind == X_TRANSLATE) {
-      h.p = h.p + v3(X.a, X.b, X.c);
-    } else {
-      h.p = rot_out(X.a, X.b, h.p);
-      h.n = rot_out(X.a, X.b, h.n);
-    }
-  }
-}
-
-// Closest t over a set of items (sphere/quad + chain), no record: the medium
-// boundary query of ConstantMedium::hit (ConstantMedium.cpp:28-32).
-__device__ __forceinline__ bool items_closest_t(const DScene &S, const DItem *its, int first, int n,
-                                                const Ray &r, double tmin, double tmax,
-                                                double &tbest) {
-  bool any = false;
-  for (int k = 0; k < n; ++k) {
-    const DItem it = its[first + k];
-    Ray lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
-    double t;
-    bool hit;
-    if (it.kind == I_SPHERE) {
-      V3 cc;
-      hit = sphere_root(S.spheres[it.idx], lr, len2(lr.d), tmin, tmax, t, cc);
-    } else {
-      hit = quad_t(S.quads[it.idx], lr, tmin, tmax, t);
-    }
-    if (hit) {
-      any = true;
-      tmax = t;
-      tbest = t;
-    }
-  }
-  return any;
-}
-
-// ConstantMedium::hit (ConstantMedium.cpp:25-94) in the medium's local frame.
-__device__ bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tmin,
-                           double tmax, Hit &h, const Key &key, uint32_t bounce) {
-  const DMedium M = S.media[it.idx];
-  Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
-  double t1, t2;
-  if (!items_closest_t(S, S.bitems, M.b_first, M.b_count, r, -kInf, kInf, t1)) return false;
-  if (!items_closest_t(S, S.bitems, M.b_first, M.b_count, r, t1 + 0.0001, kInf, t2)) return false;
-  if (t1 < tmin) t1 = tmin;
-  if (t2 > tmax) t2 = tmax;
-  if (t1 >= t2) return false;
-  if (t1 < 0) t1 = 0;
-  double rl = sqrt(len2(r.d));
-  double inside = (t2 - t1) * rl;
-  double u, unused;
-  u01x2(key, bounce, kSlotMediumBase + (uint32_t)M.id, u, unused);
-  double hd = M.neg_inv_density * log(u);
-  if (hd > inside) return false;
-  h.t = t1 + hd / rl;
-  h.p = at(r, h.t);
-  h.n = v3(1, 0, 0);
-  h.front = true;
-  h.mat = M.phase;
-  if (it.xf_count) to_world(S, it.xf_first, it.xf_count, h);
-  return true;
-}
-
-// ------------------------------------------------------------ traversal
-struct Counters {
-  uint32_t nodes, spheres, quads, other, light;
-};
-
-// Closest hit over the world BVH.  Primitive items record only (t, item) during
-// traversal and build the hit record once at the end; media build theirs when hit.
-template <bool STATS>
-__device__ __forceinline__ bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
-                                      uint32_t bounce, int *stk, Counters &cnt) {
-  const double tmin = 0.001; // Camera.cpp:242
-  double closest = kInf;
-  int best = -1;
-  bool best_full = false;
-  const double a = len2(r.d);
-  const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-
-  auto test_ref = [&](int ii) {
-    const DItem it = S.items[ii];
-    if (it.kind == I_MEDIUM) {
-      if (STATS) cnt.other++;
-      Hit tmp;
-      if (medium_hit(S, it, r, tmin, closest, tmp, key, bounce)) {
-        closest = tmp.t;
-        best = ii;
-        best_full = true;
-        h = tmp;
-      }
-      return;
-    }
-    Ray lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
-    double t;
-    bool hit;
-    if (it.kind == I_SPHERE) {
-      if (STATS) cnt.spheres++;
-      V3 cc;
-      hit = sphere_root(S.spheres[it.idx], lr, it.xf_count ? len2(lr.d) : a, tmin, closest, t, cc);
-    } else {
-      if (STATS) cnt.quads++;
-      hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
-    }
-    if (hit) {
-      closest = t;
-      best = ii;
-      best_full = false;
-    }
-  };
-
-  if (S.root_is_leaf) {
-    for (int k = 0; k < S.n_root_refs; ++k) test_ref(S.refs[k]);
-  } else {
-    int node = 0, sp = 0;
-    for (;;) {
-      if (STATS) cnt.nodes++;
-      const DNode &N = S.nodes[node];
-      double tn[2];
-      bool hit[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        double t0 = (N.lo[c][0] - r.o.x) * inv.x, t1 = (N.hi[c][0] - r.o.x) * inv.x;
-        double lo = fmin(t0, t1), hi = fmax(t0, t1);
-        t0 = (N.lo[c][1] - r.o.y) * inv.y;
-        t1 = (N.hi[c][1] - r.o.y) * inv.y;
-        lo = fmax(lo, fmin(t0, t1));
-        hi = fmin(hi, fmax(t0, t1));
-        t0 = (N.lo[c][2] - r.o.z) * inv.z;
-        t1 = (N.hi[c][2] - r.o.z) * inv.z;
-        lo = fmax(lo, fmin(t0, t1));
-        hi = fmin(hi, fmax(t0, t1));
-        lo = fmax(lo, tmin);
-        hi = fmin(hi, closest);
-        hit[c] = lo <= hi;
-        tn[c] = lo;
-      }
-      int ch0 = N.child[0], ch1 = N.child[1];
-      if (hit[0] && ch0 < 0) {
-        for (int k = 0, f = ~ch0, n = N.count[0]; k < n; ++k) test_ref(S.refs[f + k]);
-        hit[0] = false;
-      }
-      if (hit[1] && ch1 < 0) {
-        for (int k = 0, f = ~ch1, n = N.count[1]; k < n; ++k) test_ref(S.refs[f + k]);
-        hit[1] = false;
-      }
-      if (hit[0] && hit[1]) {
-        int nearc = tn[0] <= tn[1] ? ch0 : ch1;
-        int farc = tn[0] <= tn[1] ? ch1 : ch0;
-        if (sp < RT_STACK_DEPTH) stk[64 * sp++] = farc;
-        node = nearc;
-      } else if (hit[0]) {
-        node = ch0;
-      } else if (hit[1]) {
-        node = ch1;
-      } else {
-        if (sp == 0) break;
-        node = stk[64 * --sp];
-      }
-    }
-  }
-  if (best < 0) return false;
-  if (!best_full) {
-    const DItem it = S.items[best];
-    Ray lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
-    if (it.kind == I_SPHERE) {
-      const DSphere &s = S.spheres[it.idx];
-      V3 cc = v3(s.c0[0] + lr.tm * s.dir[0], s.c0[1] + lr.tm * s.dir[1], s.c0[2] + lr.tm * s.dir[2]);
-      sphere_record(s, lr, closest, cc, it.mat, h);
-    } else {
-      quad_record(S.quads[it.idx], lr, closest, it.mat, h);
-    }
-    if (it.xf_count) to_world(S, it.xf_first, it.xf_count, h);
-  }
-  return true;
-}
-
-// ------------------------------------------------------------ lights
-// Sum over light leaves of weight * pdf_value (Plane.cpp:115-126, Sphere.cpp:145-158).
-template <bool STATS>
-__device__ double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
-  double sum = 0.0;
-  for (int i = 0; i < S.n_lights; ++i) {
-    const DLight L = S.lights[i];
-    Ray lr = to_local(S, L.xf_first, L.xf_count, Ray{org, dir, 0.0});
-    double p = 0.0;
-    if (L.kind == I_SPHERE) {
-      if (STATS) cnt.light++;
-      const DSphere &s = S.spheres[L.idx];
-      double t;
-      V3 cc;
-      if (sphere_root(s, lr, len2(lr.d), 0.001, kInf, t, cc)) {
-        V3 c0 = v3(s.c0[0] + 0 * s.dir[0], s.c0[1] + 0 * s.dir[1], s.c0[2] + 0 * s.dir[2]);
-        double dist2 = len2(c0 - lr.o);
-        double ctm = sqrt(1 - s.rr / dist2);
-        double sa = 2 * kPi * (1 - ctm);
-        p = 1 / sa;
-      }
-    } else if (L.kind == I_QUAD) {
-      if (STATS) cnt.light++;
-      const DQuad &q = S.quads[L.idx];
-      double t;
-      if (quad_t(q, lr, 0.001, kInf, t)) {
-        V3 n = ld3(q.n);
-        V3 fn = dot(lr.d, n) < 0 ? n : -n;
-        double d2 = t * t * len2(lr.d);
-        double cosine = fabs(dot(lr.d, fn) / sqrt(len2(lr.d)));
-        p = d2 / (cosine * q.area);
-      }
-    }
-    sum += L.weight * p;
-  }
-  return sum;
-}
-
-__device__ V3 lights_random(const DScene &S, V3 org, double upick, double r1, double r2) {
-  int k = S.n_lights - 1;
-  for (int i = 0; i < S.n_lights; ++i)
-    if (upick < S.lights[i].cum) {
-      k = i;
-      break;
-    }
-  const DLight L = S.lights[k];
-  V3 p = to_local(S, L.xf_first, L.xf_count, Ray{org, v3(0, 0, 0), 0.0}).o;
-  V3 d;
-  if (L.kind == I_SPHERE) { // Sphere::random, Sphere.cpp:160-178
-    const DSphere &s = S.spheres[L.idx];
-    V3 c0 = v3(s.c0[0] + 0 * s.dir[0], s.c0[1] + 0 * s.dir[1], s.c0[2] + 0 * s.dir[2]);
-    V3 dir = c0 - p;
-    double d2 = len2(dir);
-    V3 w = unitv(dir);
-    V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
-    V3 vv = unitv(cross(w, a));
-    V3 uu = cross(w, vv);
-    double z = 1 + r2 * (sqrt(1 - s.rr / d2) - 1);
-    double sphi, cphi;
-    sincos(2 * kPi * r1, &sphi, &cphi);
-    double x = cphi * sqrt(1 - z * z);
-    double y = sphi * sqrt(1 - z * z);
-    d = ((x * uu) + (y * vv)) + (z * w);
-  } else if (L.kind == I_QUAD) { // Plane::random, Plane.cpp:128-132
-    const DQuad &q = S.quads[L.idx];
-    V3 pt = (ld3(q.Q) + (r1 * ld3(q.u))) + (r2 * ld3(q.v));
-    d = pt - p;
-  } else {
-    d = v3(1, 0, 0);
-  }
-  for (int c = L.xf_count - 1; c >= 0; --c) {
-    const DXform X = S.xforms[L.xf_first + c];
-    if (X.kind == X_ROTATE_Y) d = rot_out(X.a, X.b, d);
-  }
-  return d;
-}
-
-// ------------------------------------------------------------ kernel
-struct PathState {
-  Ray ray;
-  V3 T; // throughput
-  V3 L; // radiance gathered so far
-  uint32_t bounce;
-  int slot;   // tile pixel slot 0..63
-  int sample; // linear stratum index
-  bool active;
-};
-
-// One segment of Camera::ray_color in forward (throughput) form.  Returns false
-// when the path ends.
-template <bool STATS>
-__device__ bool segment(const DScene &S, const DCamera &C, PathState &ps, const Key &key, int *stk,
-                        Counters &cnt) {
-  const uint32_t b = ps.bounce;
-  Hit h;
-  if (!trace<STATS>(S, ps.ray, h, key, b, stk, cnt)) {
-    ps.L = ps.L + ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
-    return false;
-  }
-  const DMat M = S.mats[h.mat];
-  if (M.kind == RT_MAT_DIFFUSE_LIGHT) { // emits on the front face, never scatters
-    if (h.front) ps.L = ps.L + ps.T * tex_value(S, M.tex, h.p);
-    return false;
-  }
-  double e0, e1, d0, d1;
-  u01x2(key, b, kSlotEvent, e0, e1);
-  u01x2(key, b, kSlotDir, d0, d1);
-  const Ray &r = ps.ray;
-  if (M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
-    V3 refl = r.d - (2 * dot(r.d, h.n)) * h.n;
-    double z = 1.0 - 2.0 * d0;
-    double rr = sqrt(fmax(0.0, 1.0 - z * z));
-    double sp, cp;
-    sincos(2.0 * kPi * d1, &sp, &cp);
-    V3 uv = v3(rr * cp, rr * sp, z);
-    refl = unitv(refl) + (M.fuzz * uv);
-    ps.T = ps.T * ld3(M.albedo);
-    ps.ray = Ray{h.p, refl, r.tm};
-    return true;
-  }
-  if (M.kind == RT_MAT_DIELECTRIC) { // DielectricMaterial.cpp:58-85
-    double ri = h.front ? (1.0 / M.ior) : M.ior;
-    V3 ud = unitv(r.d);
-    double ct = fmin(dot(-ud, h.n), 1.0);
-    double st = sqrt(1.0 - ct * ct);
-    bool reflect_it = ri * st > 1.0;
-    if (!reflect_it) {
-      double r0 = (1 - ri) / (1 + ri);
-      r0 = r0 * r0;
-      double x = 1 - ct;
-      double x2 = x * x;
-      double refl = r0 + (1 - r0) * (x2 * x2 * x);
-      reflect_it = refl > e0;
-    }
-    V3 dir;
-    if (reflect_it) {
-      dir = ud - (2 * dot(ud, h.n)) * h.n;
-    } else {
-      V3 perp = ri * (ud + ct * h.n);
-      V3 par = (-sqrt(fabs(1.0 - len2(perp)))) * h.n;
-      dir = perp + par;
-    }
-    ps.ray = Ray{h.p, dir, r.tm};
-    return true;
-  }
-  // Lambertian (CosinePDF) or Isotropic (SpherePDF), mixed 50/50 with the lights
-  const bool lamb = (M.kind == RT_MAT_LAMBERTIAN);
-  V3 att = tex_value(S, M.tex, h.p);
-  V3 w = unitv(h.n); // ONB(n), ONB.hpp:25-37
-  V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
-  V3 ov = unitv(cross(w, a));
-  V3 ou = cross(w, ov);
-  const bool have_lights = S.n_lights > 0;
-  V3 gd;
-  if (e0 < 0.5 && have_lights) {
-    gd = lights_random(S, h.p, e1, d0, d1);
-  } else if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
-    double sp, cp;
-    sincos(2 * kPi * d0, &sp, &cp);
-    double sr = sqrt(d1);
-    V3 lc = v3(cp * sr, sp * sr, sqrt(1 - d1));
-    gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
-  } else {
-    double z = 1.0 - 2.0 * d0;
-    double rr = sqrt(fmax(0.0, 1.0 - z * z));
-    double sp, cp;
-    sincos(2.0 * kPi * d1, &sp, &cp);
-    gd = v3(rr * cp, rr * sp, z);
-  }
-  double mat_pdf;
-  if (lamb) {
-    double ct = dot(unitv(gd), w);
-    mat_pdf = fmax(0.0, ct / kPi);
-  } else {
-    mat_pdf = 1.0 / (4.0 * kPi);
-  }
-  double p0 = have_lights ? lights_pdf<STATS>(S, h.p, gd, cnt) : mat_pdf;
-  double pdf = 0.5 * p0 + 0.5 * mat_pdf;
-  double spdf;
-  if (lamb) {
-    double ct = dot(h.n, unitv(gd));
-    spdf = ct < 0 ? 0 : ct / kPi;
-  } else {
-    spdf = 1 / (4 * kPi);
-  }
-  if (spdf == 0.0 && pdf > 0.0 && pdf < kInf) return false; // zero-weight continuation
-  V3 wgt = (1 / pdf) * (spdf * att);
-  ps.T = ps.T * wgt;
-  ps.ray = Ray{h.p, gd, r.tm};
-  return true;
-}
-
-__device__ __forceinline__ Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
-  int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
-  double rs = 1.0 / C.sqrt_spp;
-  double ja, jb;
-  u01x2(key, kCamTag, 0, ja, jb);
-  double px = ((si + ja) * rs) - 0.5;
-  double py = ((sj + jb) * rs) - 0.5;
-  V3 ps = (ld3(C.p00) + ((i + px) * ld3(C.du))) + ((j + py) * ld3(C.dv)); // Camera.cpp:186-205
-  V3 org = ld3(C.center);
-  if (!(C.defocus_angle <= 0)) {
-    double a, b;
-    u01x2(key, kCamTag, 1, a, b);
-    double rr = sqrt(a);
-    double s, c;
-    sincos(2.0 * kPi * b, &s, &c);
-    double dx = rr * c, dy = rr * s;
-    org = (org + (dx * ld3(C.disk_u))) + (dy * ld3(C.disk_v)); // Camera.cpp:226-230
-  }
-  double tm, unused;
-  u01x2(key, kCamTag, 2, tm, unused);
-  return Ray{org, ps - org, tm};
-}
-
-template <bool STATS>
+template <bool STATS, unsigned F>
 __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   __shared__ int stack_lds[kWaves][RT_STACK_DEPTH][64];
@@ -649,7 +55,7 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
   acc[lane * 3 + 2] = 0.0;
 
   Counters cnt{0, 0, 0, 0, 0};
-  uint32_t n_samples = 0, n_segments = 0, n_shade = 0;
+  uint32_t n_samples = 0, n_segments = 0;
 
   const int n_items = 64 * P.sample_count;
   int next_item = 0; // wave-uniform head of the tile's work queue
@@ -685,11 +91,7 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
     if (__ballot(ps.active) == 0) break;
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS>(S, C, ps, key, stk, cnt);
-      if (cont) {
-        ps.bounce++;
-        if ((int)ps.bounce >= C.max_depth) cont = false; // depth exhausted -> 0 (Camera.cpp:236-237)
-      }
+      bool cont = segment<STATS, F>(S, C, ps, key, stk, cnt);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.L.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.L.y);
@@ -699,7 +101,6 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
     }
   }
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
   // ---- tile epilogue: one coalesced store per pixel
   {
@@ -725,7 +126,7 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
   }
   if (STATS) {
     unsigned long long v[8] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
-                               cnt.quads, cnt.other,  cnt.light, n_shade};
+                               cnt.quads, cnt.other,  cnt.light, 0};
     for (int k = 0; k < 8; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -744,6 +145,26 @@ __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint
   bytes[i] = (uint8_t)(256 * g);
 }
 
+using RenderFn = void (*)(DScene, DCamera, DLaunch, double *, unsigned long long *);
+
+const RenderFn *render_table(bool stats) {
+  static constexpr RenderFn plain[16] = {
+      render_tiles<false, 0>,  render_tiles<false, 1>,  render_tiles<false, 2>,
+      render_tiles<false, 3>,  render_tiles<false, 4>,  render_tiles<false, 5>,
+      render_tiles<false, 6>,  render_tiles<false, 7>,  render_tiles<false, 8>,
+      render_tiles<false, 9>,  render_tiles<false, 10>, render_tiles<false, 11>,
+      render_tiles<false, 12>, render_tiles<false, 13>, render_tiles<false, 14>,
+      render_tiles<false, 15>};
+  static constexpr RenderFn counted[16] = {
+      render_tiles<true, 0>,  render_tiles<true, 1>,  render_tiles<true, 2>,
+      render_tiles<true, 3>,  render_tiles<true, 4>,  render_tiles<true, 5>,
+      render_tiles<true, 6>,  render_tiles<true, 7>,  render_tiles<true, 8>,
+      render_tiles<true, 9>,  render_tiles<true, 10>, render_tiles<true, 11>,
+      render_tiles<true, 12>, render_tiles<true, 13>, render_tiles<true, 14>,
+      render_tiles<true, 15>};
+  return stats ? counted : plain;
+}
+
 } // namespace
 
 // ---------------------------------------------------------------- launchers
@@ -753,12 +174,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   int n_tiles = P->tiles_x * P->tiles_y;
   int blocks = (n_tiles + kWaves - 1) / kWaves;
   if (blocks == 0) return hipSuccess;
-  if (stats)
-    hipLaunchKernelGGL(render_tiles<true>, dim3(blocks), dim3(64 * kWaves), 0, stream, *S, *C, *P,
-                       out, stats);
-  else
-    hipLaunchKernelGGL(render_tiles<false>, dim3(blocks), dim3(64 * kWaves), 0, stream, *S, *C, *P,
-                       out, nullptr);
+  RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), 0, stream, *S, *C, *P, out, stats);
   return hipGetLastError();
 }
 
@@ -770,3 +187,4 @@ extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double s
   hipLaunchKernelGGL(to_bytes_kernel, dim3(blocks), dim3(256), 0, stream, rgb, n, scale, bytes);
   return hipGetLastError();
 }
+

@@ -123,7 +123,15 @@ struct DScene {      // kernel argument (by value)
   int32_t n_nodes;
   int32_t root_is_leaf;  // whole world is one leaf: refs [0, n_root_refs)
   int32_t n_root_refs;
+  int32_t features;      // RT_FEAT_* bits: selects the specialised kernel instance
+  int32_t pad;
 };
+
+// Scene features (kernel specialisation keys)
+#define RT_FEAT_MEDIA 1  // constant media among the world items
+#define RT_FEAT_XFORM 2  // transform chains on world items or lights
+#define RT_FEAT_LIGHTS 4 // non-empty light list
+#define RT_FEAT_NOISE 8  // Perlin noise textures
 
 struct DCamera {     // the rt_frame values the kernel needs
   double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
