@@ -129,38 +129,60 @@ def main():
     s0 = rank * n_strata // ws
     s1 = (rank + 1) * n_strata // ws
 
+    from rtx.dist import ShardedRenderer, max_over_ranks
     R = Renderer(scene, device=local)
     info = R.info()
-    acc = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # two accumulators: the RCCL reduce of frame k overlaps the render of k+1
+    accs = [torch.zeros((H, W, 3), dtype=torch.float64, device=dev) for _ in range(2)]
+    pending = [None, None]
 
-    def step(seed):
+    def render_fn(fr, acc, seed, strata):
         # each rank overwrites its partial sums (no memset, no read-modify-write)
-        R.render_device(frame, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=(s0, s1 - s0),
+        R.render_device(fr, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=strata,
                         output=abi.RT_OUT_SUM, accumulate=0)
+
+    sharded = ShardedRenderer(render_fn, frame, rank, ws)
+    assert sharded.strata == (s0, s1)
+    kernel_ms = []
+
+    def step(k, seed):
+        b = k % 2
+        if pending[b] is not None:  # buffer still being reduced from step k-2
+            pending[b].wait()
+            pending[b] = None
+        render_fn(frame, accs[b], seed, (s0, s1 - s0))
         if ws > 1:
-            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+            pending[b] = dist.reduce(accs[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for w in range(args.warmup):
-        step(1000 + w)
+        step(w, 1000 + w)
+    drain()
     torch.cuda.synchronize(dev)
 
-    kernel_ms = []
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
-        kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
+        step(k, k)
+        if ws == 1:
+            kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
+    drain()
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    if ws > 1:  # kernel time measured after the timed region (no sync inside it)
+        for k in range(min(2, args.steps)):
+            render_fn(frame, accs[0], 5000 + k, (s0, s1 - s0))
+            kernel_ms.append(R.last_kernel_ms())
 
     samples_per_step = W * H * n_strata  # whole frame, all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
