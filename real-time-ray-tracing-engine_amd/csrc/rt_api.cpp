@@ -174,7 +174,6 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     return parts.size() - 1;
   };
   size_t iN = add(H.nodes.data(), H.nodes.size() * sizeof(DNode));
-  size_t iR = add(H.refs.data(), H.refs.size() * sizeof(int32_t));
   size_t iI = add(H.items.data(), H.items.size() * sizeof(DItem));
   size_t iB = add(H.bitems.data(), H.bitems.size() * sizeof(DItem));
   size_t iX = add(H.xforms.data(), H.xforms.size() * sizeof(DXform));
@@ -213,7 +212,6 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   auto P = [&](size_t i) { return (const void *)(s->block + parts[i].off); };
   DScene &d = s->ds;
   d.nodes = (const DNode *)P(iN);
-  d.refs = (const int32_t *)P(iR);
   d.items = (const DItem *)P(iI);
   d.bitems = (const DItem *)P(iB);
   d.xforms = (const DXform *)P(iX);
@@ -227,7 +225,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   d.n_lights = (int32_t)H.lights.size();
   d.n_nodes = (int32_t)H.nodes.size();
   d.root_is_leaf = H.root_is_leaf;
-  d.n_root_refs = H.n_root_refs;
+  d.n_root_items = H.n_root_items;
   d.features = 0;
   for (const DItem &it : H.items) {
     if (it.kind == I_MEDIUM) d.features |= RT_FEAT_MEDIA;
@@ -246,7 +244,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   rt_scene_info &in = s->info;
   std::memset(&in, 0, sizeof in);
   in.n_nodes = (int32_t)H.nodes.size();
-  in.n_leaf_refs = (int32_t)H.refs.size();
+  in.n_leaf_refs = (int32_t)H.items.size(); // leaves are item ranges
   in.n_spheres = (int32_t)H.spheres.size();
   in.n_quads = (int32_t)H.quads.size();
   in.n_objects = (int32_t)H.items.size();

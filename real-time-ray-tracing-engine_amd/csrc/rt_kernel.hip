@@ -35,8 +35,14 @@ namespace {
 using namespace rtp;
 constexpr int kWaves = 4; // waves (tiles) per 256-thread block
 
+#ifdef RT_WAVES_PER_EU
+#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+#else
+#define RT_OCCUPANCY
+#endif
+
 template <bool STATS, unsigned F>
-__global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(256) RT_OCCUPANCY void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   __shared__ int stack_lds[kWaves][RT_STACK_DEPTH][64];
   __shared__ double acc_lds[kWaves][64][3];
@@ -54,7 +60,7 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
   acc[lane * 3 + 1] = 0.0;
   acc[lane * 3 + 2] = 0.0;
 
-  Counters cnt{0, 0, 0, 0, 0};
+  Counters cnt{0, 0, 0, 0, 0, 0};
   uint32_t n_samples = 0, n_segments = 0;
 
   const int n_items = 64 * P.sample_count;
@@ -126,7 +132,7 @@ __global__ __launch_bounds__(256) void render_tiles(DScene S, DCamera C, DLaunch
   }
   if (STATS) {
     unsigned long long v[8] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
-                               cnt.quads, cnt.other,  cnt.light, 0};
+                               cnt.quads, cnt.other,  cnt.light, cnt.shade};
     for (int k = 0; k < 8; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);

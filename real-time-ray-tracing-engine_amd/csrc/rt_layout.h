@@ -13,11 +13,14 @@
 // medium keeps its boundary as a range of items in the medium's local frame.
 // The device code therefore needs no recursion and no function calls.
 //
-//   - world BVH: binary nodes carrying BOTH children's boxes (one 128-B fetch
-//     tests two boxes), children by index, leaves as ranges of item references;
+//   - world BVH: binary nodes carrying BOTH children's boxes (one 64-B fetch
+//     tests two boxes), children by index, leaves as ranges of items (the item
+//     array is permuted into leaf order, so there is no reference indirection);
+//     boxes are fp32 rounded outward and tested conservatively (rt_path.h), the
+//     primitive tests that decide every hit stay fp64;
 //   - lights: flattened to weighted leaves (primitive + transform chain), so light
 //     sampling and the light pdf are plain loops.
-// Everything is fp64, matching the reference arithmetic (Vec3.hpp:184).
+// Everything but the BVH boxes is fp64, matching the reference arithmetic (Vec3.hpp:184).
 #ifndef RT_LAYOUT_H
 #define RT_LAYOUT_H
 #include <stdint.h>
@@ -70,12 +73,12 @@ struct DMedium {     // ConstantMedium: -1/density, phase material, boundary ite
   int32_t b_first, b_count; // boundary items in bitems[] (medium-local frame)
 };
 
-struct DNode {       // 128 B: both children's boxes + links
-  double lo[2][3];
-  double hi[2][3];
-  int32_t child[2];  // >= 0 inner node index; < 0: leaf, refs at ~child
-  int32_t count[2];  // leaf ref count, 0 for inner children
-  int32_t pad[4];
+struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + links
+  float lo0[3], hi0[3];
+  float lo1[3], hi1[3];
+  int32_t entry[2];  // >= 0: inner node index; < 0: leaf ~((first << 3) | count),
+                     // items [first, first + count) (items are stored in leaf order)
+  int32_t pad[2];
 };
 
 struct DMat {        // 48 B
@@ -108,8 +111,7 @@ struct DLight {      // flattened light leaf (48 B)
 
 struct DScene {      // kernel argument (by value)
   const DNode *nodes;
-  const int32_t *refs;   // leaf item references
-  const DItem *items;    // world items
+  const DItem *items;    // world items, in BVH leaf order
   const DItem *bitems;   // medium boundary items
   const DXform *xforms;
   const DSphere *spheres;
@@ -121,8 +123,8 @@ struct DScene {      // kernel argument (by value)
   const DLight *lights;
   int32_t n_lights;
   int32_t n_nodes;
-  int32_t root_is_leaf;  // whole world is one leaf: refs [0, n_root_refs)
-  int32_t n_root_refs;
+  int32_t root_is_leaf;  // whole world is one leaf: items [0, n_root_items)
+  int32_t n_root_items;
   int32_t features;      // RT_FEAT_* bits: selects the specialised kernel instance
   int32_t pad;
 };

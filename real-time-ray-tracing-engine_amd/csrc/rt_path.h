@@ -309,14 +309,71 @@ RT_HD bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tm
 }
 
 // ------------------------------------------------------------ traversal
+// Conservative fp32 slab test.  Node boxes are fp32 rounded outward with a
+// relative 2^-20 + 1e-7 margin (rt_scene.cpp); per ray the origin is rounded up
+// for the lo planes and down for the hi planes, so (lo - o) and (hi - o) are
+// bracketed before the fp32 subtraction/multiply, whose relative error (< 4
+// ulp) the 1 + 2^-20 growth of the far distance absorbs (Ize, "Robust BVH Ray
+// Traversal", JCGT 2013).  A box can thus only be visited MORE often than under
+// exact arithmetic, never less; every hit is still decided by the fp64
+// primitive tests, so the closest hit is unchanged.
+RT_HD RT_FI uint32_t f32_bits(float f) {
+  union {
+    float f;
+    uint32_t u;
+  } x{f};
+  return x.u;
+}
+RT_HD RT_FI float f32_from(uint32_t u) {
+  union {
+    uint32_t u;
+    float f;
+  } x{u};
+  return x.f;
+}
+RT_HD RT_FI float f32_up(double x) { // smallest float >= x (x not NaN)
+  float f = (float)x;
+  if ((double)f < x) f = (f == 0.0f) ? f32_from(1u) : f32_from(f > 0.0f ? f32_bits(f) + 1u : f32_bits(f) - 1u);
+  return f;
+}
+RT_HD RT_FI float f32_dn(double x) { // largest float <= x (x not NaN)
+  float f = (float)x;
+  if ((double)f > x) f = (f == 0.0f) ? f32_from(0x80000001u) : f32_from(f > 0.0f ? f32_bits(f) - 1u : f32_bits(f) + 1u);
+  return f;
+}
+constexpr float kSlabGrow = 1.0f + 0x1p-20f;
+constexpr float kInvClamp = 1e30f; // finite 1/d: a 0 * inf NaN would drop a box
+
+struct RayF { // per-ray fp32 slab-test constants
+  float oa[3], ob[3], inv[3];
+};
+RT_HD RT_FI RayF ray_f32(const Ray &r) {
+  RayF q;
+  const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    q.oa[a] = f32_up(o[a]);
+    q.ob[a] = f32_dn(o[a]);
+    float iv = (float)(1.0 / d[a]);
+    q.inv[a] = fminf(fmaxf(iv, -kInvClamp), kInvClamp);
+  }
+  return q;
+}
+// Entry distance if the ray may hit [lo,hi] within [tmin32, cl32], else +inf.
+RT_HD RT_FI float slab(const RayF &q, const float *lo, const float *hi, float tmin32, float cl32) {
+  float a0 = (lo[0] - q.oa[0]) * q.inv[0], b0 = (hi[0] - q.ob[0]) * q.inv[0];
+  float a1 = (lo[1] - q.oa[1]) * q.inv[1], b1 = (hi[1] - q.ob[1]) * q.inv[1];
+  float a2 = (lo[2] - q.oa[2]) * q.inv[2], b2 = (hi[2] - q.ob[2]) * q.inv[2];
+  float tl = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), tmin32));
+  float th = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), cl32));
+  return tl <= th * kSlabGrow ? tl : __builtin_huge_valf();
+}
+
 struct Counters {
-  uint32_t nodes, spheres, quads, other, light;
+  uint32_t nodes, spheres, quads, other, light, shade;
 };
 
-// Stack / queue entry: >= 0 inner node; < 0 a leaf ~(first << 3 | count).
-RT_HD RT_FI int leaf_entry(int child_field, int count) {
-  return ~(((~child_field) << 3) | count);
-}
+// Stack entry: >= 0 inner node; < 0 a leaf ~(first << 3 | count) (DNode::entry).
 
 // Closest hit over the world BVH.  Primitive items record only (t, item) during
 // traversal and build the hit record once at the end; media build theirs when hit.
@@ -328,7 +385,9 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   int best = -1;
   bool best_full = false;
   const double a = len2(r.d);
-  const V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+  const RayF q = ray_f32(r);
+  const float tmin32 = f32_dn(tmin);
+  float cl32 = __builtin_huge_valf(); // f32_up(closest)
 
   int sp = 0;
   int cur;   // current entry: node (>= 0) or leaf (< 0)
@@ -336,7 +395,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   if (S.root_is_leaf) {
     cur = -1;
     lf = 0;
-    ln = S.n_root_refs;
+    ln = S.n_root_items;
   } else {
     cur = 0;
   }
@@ -357,34 +416,17 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       // ---- inner node: test both children's boxes
       if (STATS) cnt.nodes++;
       const DNode &N = S.nodes[cur];
-      double tn[2];
-      bool hit[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        double t0 = (N.lo[c][0] - r.o.x) * inv.x, t1 = (N.hi[c][0] - r.o.x) * inv.x;
-        double lo = fmin(t0, t1), hi = fmax(t0, t1);
-        t0 = (N.lo[c][1] - r.o.y) * inv.y;
-        t1 = (N.hi[c][1] - r.o.y) * inv.y;
-        lo = fmax(lo, fmin(t0, t1));
-        hi = fmin(hi, fmax(t0, t1));
-        t0 = (N.lo[c][2] - r.o.z) * inv.z;
-        t1 = (N.hi[c][2] - r.o.z) * inv.z;
-        lo = fmax(lo, fmin(t0, t1));
-        hi = fmin(hi, fmax(t0, t1));
-        lo = fmax(lo, tmin);
-        hi = fmin(hi, closest);
-        hit[c] = lo <= hi;
-        tn[c] = lo;
-      }
-      int e0 = N.child[0] >= 0 ? N.child[0] : leaf_entry(N.child[0], N.count[0]);
-      int e1 = N.child[1] >= 0 ? N.child[1] : leaf_entry(N.child[1], N.count[1]);
-      if (hit[0] && hit[1]) {
-        bool first0 = tn[0] <= tn[1];
+      const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
+      const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
+      const int e0 = N.entry[0], e1 = N.entry[1];
+      const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
+      if (h0 && h1) {
+        bool first0 = tn0 <= tn1;
         if (sp < RT_STACK_DEPTH) stk[64 * sp++] = first0 ? e1 : e0;
         cur = first0 ? e0 : e1;
-      } else if (hit[0]) {
+      } else if (h0) {
         cur = e0;
-      } else if (hit[1]) {
+      } else if (h1) {
         cur = e1;
       } else {
         cur = -1;
@@ -398,7 +440,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     }
     if (ln == 0) break; // stack empty and no pending leaf: done
     while (ln > 0) { // ---- the single leaf-test site
-      const int ii = S.refs[lf];
+      const int ii = lf;
       ++lf;
       --ln;
       const DItem it = S.items[ii];
@@ -408,6 +450,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           Hit tmp;
           if (medium_hit(S, it, r, tmin, closest, tmp, key, bounce)) {
             closest = tmp.t;
+            cl32 = f32_up(closest);
             best = ii;
             best_full = true;
             h = tmp;
@@ -434,6 +477,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       }
       if (hit) {
         closest = t;
+        cl32 = f32_up(closest);
         best = ii;
         best_full = false;
       }
@@ -567,6 +611,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     return false;
   }
   const DMat M = S.mats[h.mat];
+  if (STATS) cnt.shade++;
   if (M.kind == RT_MAT_DIFFUSE_LIGHT) { // emits on the front face, never scatters
     // Always add T * emitted (0 on the back face): a NaN/inf throughput must
     // poison the sample as the reference recursion does (NaN * 0 = NaN).

@@ -587,6 +587,22 @@ struct Compiler {
     return id;
   }
 
+  // fp32 box bounds rounded outward, widened by a relative 2^-20 plus 1e-7 so
+  // the conservative fp32 slab test (rt_path.h) can never reject a box whose
+  // primitives the fp64 test would hit.
+  static float f32_lo(double x) {
+    double m = x - (std::fabs(x) * 0x1p-20 + 1e-7);
+    float f = (float)m;
+    if ((double)f > m) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+  }
+  static float f32_hi(double x) {
+    double m = x + (std::fabs(x) * 0x1p-20 + 1e-7);
+    float f = (float)m;
+    if ((double)f < m) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+  }
+
   void emit_world_bvh(const std::vector<Bx> &item_box) {
     std::vector<BRef> r;
     for (size_t i = 0; i < item_box.size(); ++i) {
@@ -598,16 +614,20 @@ struct Compiler {
     }
     if (r.empty()) {
       H.root_is_leaf = 1;
-      H.n_root_refs = 0;
+      H.n_root_items = 0;
       return;
     }
     bn.clear();
     int root = build(r, 0, (int)r.size(), 0);
     H.bvh_depth = max_depth_seen;
-    for (auto &x : r) H.refs.push_back(x.obj);
+    // store the items in leaf order: a leaf is a contiguous item range
+    std::vector<DItem> leaf_order;
+    leaf_order.reserve(r.size());
+    for (auto &x : r) leaf_order.push_back(H.items[x.obj]);
+    H.items.swap(leaf_order);
     if (bn[root].left < 0) {
       H.root_is_leaf = 1;
-      H.n_root_refs = bn[root].count;
+      H.n_root_items = bn[root].count;
       return;
     }
     // flatten: DFS over inner build nodes; each DNode holds both children's boxes
@@ -629,17 +649,12 @@ struct Compiler {
       int ch[2] = {p.left, p.right};
       for (int k = 0; k < 2; ++k) {
         const BNode &c = bn[ch[k]];
+        float *lo = k ? d.lo1 : d.lo0, *hi = k ? d.hi1 : d.hi0;
         for (int a = 0; a < 3; ++a) {
-          d.lo[k][a] = c.b.lo[a];
-          d.hi[k][a] = c.b.hi[a];
+          lo[a] = f32_lo(c.b.lo[a]);
+          hi[a] = f32_hi(c.b.hi[a]);
         }
-        if (c.left < 0) {
-          d.child[k] = ~c.first;
-          d.count[k] = c.count;
-        } else {
-          d.child[k] = map[ch[k]];
-          d.count[k] = 0;
-        }
+        d.entry[k] = c.left < 0 ? ~((c.first << 3) | c.count) : map[ch[k]];
       }
     }
   }

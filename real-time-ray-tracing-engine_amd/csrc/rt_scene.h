@@ -11,7 +11,6 @@ namespace rtx {
 
 struct HostScene {
   std::vector<DNode> nodes;
-  std::vector<int32_t> refs;
   std::vector<DItem> items;
   std::vector<DItem> bitems;
   std::vector<DXform> xforms;
@@ -23,7 +22,7 @@ struct HostScene {
   std::vector<DPerlin> perlin;
   std::vector<DLight> lights;
   int32_t root_is_leaf = 0;
-  int32_t n_root_refs = 0;
+  int32_t n_root_items = 0;
   int32_t bvh_depth = 0;
 };
 

@@ -21,7 +21,7 @@ namespace {
 template <unsigned F>
 void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, int i, int j,
                  int s0, int s1, int *stk, double acc[3]) {
-  Counters cnt{0, 0, 0, 0, 0};
+  Counters cnt{0, 0, 0, 0, 0, 0};
   for (int k = s0; k < s1; ++k) {
     Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)(j * C.W + i), (uint32_t)k};
     PathState ps;
@@ -58,7 +58,6 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   if (rtx::compile_scene(desc, H, err) != RT_OK) return -1;
   DScene S;
   S.nodes = H.nodes.data();
-  S.refs = H.refs.data();
   S.items = H.items.data();
   S.bitems = H.bitems.data();
   S.xforms = H.xforms.data();
@@ -72,7 +71,7 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   S.n_lights = (int32_t)H.lights.size();
   S.n_nodes = (int32_t)H.nodes.size();
   S.root_is_leaf = H.root_is_leaf;
-  S.n_root_refs = H.n_root_refs;
+  S.n_root_items = H.n_root_items;
   S.features = features;
   DCamera C;
   auto cp = [](double *d, const rt_vec3 &v) {

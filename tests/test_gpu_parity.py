@@ -150,6 +150,8 @@ def test_stats_counters_are_consistent():
     assert st["samples"] == f.image_width * f.image_height * 4
     assert st["samples"] <= st["segments"] <= 8 * st["samples"]
     assert st["node_visits"] > st["segments"]
+    # every segment either misses (sky) or shades one hit
+    assert 0 < st["shade_events"] <= st["segments"]
     assert info["n_spheres"] == 486 and info["bvh_depth"] < 30
 
 
