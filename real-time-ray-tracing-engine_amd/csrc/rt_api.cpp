@@ -176,6 +176,8 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   size_t iN = add(H.nodes.data(), H.nodes.size() * sizeof(DNode));
   size_t iI = add(H.items.data(), H.items.size() * sizeof(DItem));
   size_t iB = add(H.bitems.data(), H.bitems.size() * sizeof(DItem));
+  size_t iMI = add(H.mitems.data(), H.mitems.size() * sizeof(DItem));
+  size_t iMB = add(H.mbox.data(), H.mbox.size() * sizeof(float));
   size_t iX = add(H.xforms.data(), H.xforms.size() * sizeof(DXform));
   size_t iS = add(H.spheres.data(), H.spheres.size() * sizeof(DSphere));
   size_t iQ = add(H.quads.data(), H.quads.size() * sizeof(DQuad));
@@ -214,6 +216,9 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   d.nodes = (const DNode *)P(iN);
   d.items = (const DItem *)P(iI);
   d.bitems = (const DItem *)P(iB);
+  d.mitems = (const DItem *)P(iMI);
+  d.mbox = (const float *)P(iMB);
+  d.n_mitems = (int32_t)H.mitems.size();
   d.xforms = (const DXform *)P(iX);
   d.spheres = (const DSphere *)P(iS);
   d.quads = (const DQuad *)P(iQ);
@@ -227,10 +232,11 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   d.root_is_leaf = H.root_is_leaf;
   d.n_root_items = H.n_root_items;
   d.features = 0;
-  for (const DItem &it : H.items) {
-    if (it.kind == I_MEDIUM) d.features |= RT_FEAT_MEDIA;
+  if (!H.mitems.empty()) d.features |= RT_FEAT_MEDIA;
+  for (const DItem &it : H.items)
     if (it.xf_count) d.features |= RT_FEAT_XFORM;
-  }
+  for (const DItem &it : H.mitems)
+    if (it.xf_count) d.features |= RT_FEAT_XFORM;
   for (const DLight &L : H.lights)
     if (L.xf_count) d.features |= RT_FEAT_XFORM;
   if (!H.lights.empty()) d.features |= RT_FEAT_LIGHTS;
@@ -238,7 +244,6 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
   if (const char *fx = std::getenv("RTX_EXTRA_FEATURES")) // debug: widen the instance
     d.features |= std::atoi(fx) & 15;
-  d.pad = 0;
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
 
   rt_scene_info &in = s->info;
@@ -247,7 +252,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.n_leaf_refs = (int32_t)H.items.size(); // leaves are item ranges
   in.n_spheres = (int32_t)H.spheres.size();
   in.n_quads = (int32_t)H.quads.size();
-  in.n_objects = (int32_t)H.items.size();
+  in.n_objects = (int32_t)(H.items.size() + H.mitems.size());
   in.n_light_leaves = (int32_t)H.lights.size();
   in.bvh_depth = H.bvh_depth;
   in.node_bytes = (int32_t)sizeof(DNode);

@@ -111,7 +111,9 @@ struct DLight {      // flattened light leaf (48 B)
 
 struct DScene {      // kernel argument (by value)
   const DNode *nodes;
-  const DItem *items;    // world items, in BVH leaf order
+  const DItem *items;    // world primitive items, in BVH leaf order
+  const DItem *mitems;   // world media (tested after the BVH walk, see rt_path.h)
+  const float *mbox;     // per medium: world box lo[3], hi[3] (fp32, rounded outward)
   const DItem *bitems;   // medium boundary items
   const DXform *xforms;
   const DSphere *spheres;
@@ -126,7 +128,7 @@ struct DScene {      // kernel argument (by value)
   int32_t root_is_leaf;  // whole world is one leaf: items [0, n_root_items)
   int32_t n_root_items;
   int32_t features;      // RT_FEAT_* bits: selects the specialised kernel instance
-  int32_t pad;
+  int32_t n_mitems;
 };
 
 // Scene features (kernel specialisation keys)

@@ -257,11 +257,11 @@ RT_HD RT_FI void to_world(const DScene &S, int f, int n, Hit &h) {
   }
 }
 
-// Closest t over a set of items (sphere/quad + chain), no record: the medium
-// boundary query of ConstantMedium::hit (ConstantMedium.cpp:28-32).
-RT_HD RT_FI bool items_closest_t(const DScene &S, const DItem *its, int first, int n,
-                                                const Ray &r, double tmin, double tmax,
-                                                double &tbest) {
+// Closest t over a set of items (sphere/quad + chain), no record: one boundary
+// query of ConstantMedium::hit (ConstantMedium.cpp:28-32).  Used only as the
+// fallback of boundary_span.
+RT_HD bool items_closest_t(const DScene &S, const DItem *its, int first, int n, const Ray &r,
+                           double tmin, double tmax, double &tbest) {
   bool any = false;
   for (int k = 0; k < n; ++k) {
     const DItem it = its[first + k];
@@ -281,14 +281,90 @@ RT_HD RT_FI bool items_closest_t(const DScene &S, const DItem *its, int first, i
   return any;
 }
 
+// Both boundary queries of ConstantMedium::hit in ONE pass over the boundary
+// items: t1 = closest boundary hit on (-inf, inf), t2 = closest beyond t1+1e-4
+// (ConstantMedium.cpp:28-32).  A scan's result is the minimum over the items'
+// distances that pass its interval test (a sphere offers both roots, open
+// interval; a quad its plane distance, closed interval), so the three smallest
+// candidates decide both; only when more than three candidates exist and none
+// of the kept ones passes the second test does the exact second scan run.
+RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, double &t1,
+                               double &t2) {
+  // the three smallest candidates, ascending; kK: quad candidate (closed interval)
+  double c0 = 0, c1 = 0, c2 = 0;
+  bool k0 = false, k1 = false, k2 = false;
+  int n_cand = 0;
+  auto keep = [&](double t, bool cl) {
+    ++n_cand;
+    if (n_cand == 1 || t < c0) {
+      c2 = c1, k2 = k1, c1 = c0, k1 = k0, c0 = t, k0 = cl;
+    } else if (n_cand == 2 || t < c1) {
+      c2 = c1, k2 = k1, c1 = t, k1 = cl;
+    } else if (n_cand == 3 || t < c2) {
+      c2 = t, k2 = cl;
+    }
+  };
+  for (int k = 0; k < M.b_count; ++k) {
+    const DItem it = S.bitems[M.b_first + k];
+    Ray lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
+    if (it.kind == I_SPHERE) { // sphere_root's two roots
+      const DSphere &sp = S.spheres[it.idx];
+      V3 cc = v3(sp.c0[0] + lr.tm * sp.dir[0], sp.c0[1] + lr.tm * sp.dir[1],
+                 sp.c0[2] + lr.tm * sp.dir[2]);
+      V3 oc = cc - lr.o;
+      double a = len2(lr.d);
+      double h = dot(lr.d, oc);
+      double cc2 = len2(oc) - sp.rr;
+      double disc = h * h - a * cc2;
+      if (disc < 0) continue;
+      double sq = sqrt(disc);
+      double r1 = (h - sq) / a, r2 = (h + sq) / a;
+      if (-kInf < r1 && r1 < kInf) keep(r1, false);
+      if (-kInf < r2 && r2 < kInf) keep(r2, false);
+    } else { // quad_t without its interval test
+      const DQuad &q = S.quads[it.idx];
+      V3 n = ld3(q.n);
+      double denom = dot(n, lr.d);
+      if (fabs(denom) < 1e-8) continue;
+      double tt = (q.D - dot(n, lr.o)) / denom;
+      if (!(-kInf <= tt && tt <= kInf)) continue;
+      V3 pv = at(lr, tt) - ld3(q.Q);
+      V3 w = ld3(q.w);
+      double alpha = dot(w, cross(pv, ld3(q.v)));
+      double beta = dot(w, cross(ld3(q.u), pv));
+      if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) continue;
+      keep(tt, true);
+    }
+  }
+  if (n_cand == 0) return false;
+  t1 = c0;
+  const double thr = t1 + 0.0001;
+  auto pass = [&](double t, bool cl) {
+    return cl ? (thr <= t && t <= kInf) : (thr < t && t < kInf);
+  };
+  if (pass(c0, k0)) {
+    t2 = c0;
+    return true;
+  }
+  if (n_cand >= 2 && pass(c1, k1)) {
+    t2 = c1;
+    return true;
+  }
+  if (n_cand >= 3 && pass(c2, k2)) {
+    t2 = c2;
+    return true;
+  }
+  if (n_cand <= 3) return false;
+  return items_closest_t(S, S.bitems, M.b_first, M.b_count, r, thr, kInf, t2);
+}
+
 // ConstantMedium::hit (ConstantMedium.cpp:25-94) in the medium's local frame.
 RT_HD bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tmin,
                            double tmax, Hit &h, const Key &key, uint32_t bounce) {
   const DMedium M = S.media[it.idx];
   Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
   double t1, t2;
-  if (!items_closest_t(S, S.bitems, M.b_first, M.b_count, r, -kInf, kInf, t1)) return false;
-  if (!items_closest_t(S, S.bitems, M.b_first, M.b_count, r, t1 + 0.0001, kInf, t2)) return false;
+  if (!boundary_span(S, M, r, t1, t2)) return false;
   if (t1 < tmin) t1 = tmin;
   if (t2 > tmax) t2 = tmax;
   if (t1 >= t2) return false;
@@ -444,20 +520,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       ++lf;
       --ln;
       const DItem it = S.items[ii];
-      if constexpr ((F & F_MEDIA) != 0) {
-        if (it.kind == I_MEDIUM) {
-          if (STATS) cnt.other++;
-          Hit tmp;
-          if (medium_hit(S, it, r, tmin, closest, tmp, key, bounce)) {
-            closest = tmp.t;
-            cl32 = f32_up(closest);
-            best = ii;
-            best_full = true;
-            h = tmp;
-          }
-          continue;
-        }
-      }
       Ray lr = r;
       double al = a;
       if constexpr ((F & F_XFORM) != 0) {
@@ -480,6 +542,25 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         cl32 = f32_up(closest);
         best = ii;
         best_full = false;
+      }
+    }
+  }
+  // Media after the BVH walk, against the final primitive distance: the closest
+  // hit is the minimum over items either way, and a medium's draw is keyed by
+  // its id, not by visiting order.  Keeps the medium code out of the traversal
+  // loop's register budget.
+  if constexpr ((F & F_MEDIA) != 0) {
+    for (int m = 0; m < S.n_mitems; ++m) {
+      if (slab(q, S.mbox + 6 * m, S.mbox + 6 * m + 3, tmin32, cl32) == __builtin_huge_valf())
+        continue;
+      if (STATS) cnt.other++;
+      Hit tmp;
+      if (medium_hit(S, S.mitems[m], r, tmin, closest, tmp, key, bounce)) {
+        closest = tmp.t;
+        cl32 = f32_up(closest);
+        best = m;
+        best_full = true;
+        h = tmp;
       }
     }
   }

@@ -826,6 +826,12 @@ struct Compiler {
       DItem it;
       Bx bb;
       if (!make_item(f, it, bb)) return false;
+      if (it.kind == I_MEDIUM) {
+        H.mitems.push_back(it);
+        for (int a = 0; a < 3; ++a) H.mbox.push_back(f32_lo(bb.lo[a]));
+        for (int a = 0; a < 3; ++a) H.mbox.push_back(f32_hi(bb.hi[a]));
+        continue;
+      }
       H.items.push_back(it);
       ibox.push_back(bb);
     }

@@ -12,6 +12,8 @@ namespace rtx {
 struct HostScene {
   std::vector<DNode> nodes;
   std::vector<DItem> items;
+  std::vector<DItem> mitems; // media (not in the BVH)
+  std::vector<float> mbox;   // 6 per medium
   std::vector<DItem> bitems;
   std::vector<DXform> xforms;
   std::vector<DSphere> spheres;

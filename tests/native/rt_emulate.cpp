@@ -60,6 +60,9 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   S.nodes = H.nodes.data();
   S.items = H.items.data();
   S.bitems = H.bitems.data();
+  S.mitems = H.mitems.data();
+  S.mbox = H.mbox.data();
+  S.n_mitems = (int32_t)H.mitems.size();
   S.xforms = H.xforms.data();
   S.spheres = H.spheres.data();
   S.quads = H.quads.data();
