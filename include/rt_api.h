@@ -111,6 +111,8 @@ enum {
   RT_OBJ_MEDIUM = 5     /* ConstantMedium             ConstantMedium.cpp:25-94 */
 };
 
+#define RT_STORED_FORM 2
+
 typedef struct rt_object_desc {
   int32_t kind;
   int32_t material; /* sphere / quad: material index, -1 = none (light-list entries) */
@@ -121,7 +123,13 @@ typedef struct rt_object_desc {
   rt_vec3 b;        /* sphere: centre at t=1 (moving only);  quad: side u */
   rt_vec3 c;        /* quad: side v */
   double s;         /* sphere: radius;  rotate_y: angle in degrees;  medium: density */
-  int32_t moving;   /* sphere: 1 = two-centre constructor (Sphere.cpp:15-23) */
+  int32_t moving;   /* sphere: 0 static; 1 = two-centre constructor, b = centre at t=1
+                       (Sphere.cpp:15-23); RT_STORED_FORM = b is the stored displacement
+                       c1 - c0 (Sphere::get_center().direction()).
+                       rotate_y: RT_STORED_FORM = (a.x, a.y) are the stored (sin, cos)
+                       (RotateY.hpp m_sin_theta/m_cos_theta) instead of s degrees.
+                       The stored forms let a binding hand over the reference objects'
+                       own doubles without a lossy round trip. */
   int32_t phase;    /* medium: material index of the phase function (isotropic) */
 } rt_object_desc;
 

@@ -1008,10 +1008,9 @@ Obj *Builder::build(int idx) {
     V c0 = from(d.a);
     o->radius = std::fmax(0, d.s);
     V rv = mk(d.s, d.s, d.s);
-    if (d.moving) { // Sphere.cpp:15-23
-      V c1 = from(d.b);
+    if (d.moving) { // Sphere.cpp:15-23 (RT_STORED_FORM: b is c1 - c0 itself)
       o->c0 = c0;
-      o->cdir = c1 - c0;
+      o->cdir = d.moving == RT_STORED_FORM ? from(d.b) : from(d.b) - c0;
       V a0 = mk(o->c0.x + 0 * o->cdir.x, o->c0.y + 0 * o->cdir.y, o->c0.z + 0 * o->cdir.z);
       V a1 = mk(o->c0.x + 1 * o->cdir.x, o->c0.y + 1 * o->cdir.y, o->c0.z + 1 * o->cdir.z);
       o->bbox = box_join(box_pts(a0 - rv, a0 + rv), box_pts(a1 - rv, a1 + rv));
@@ -1054,9 +1053,14 @@ Obj *Builder::build(int idx) {
     Obj *c = build(d.child);
     if (!c) return nullptr;
     o->kids = {c};
-    double rad = d.s * PI / 180.0;
-    o->sin_t = std::sin(rad);
-    o->cos_t = std::cos(rad);
+    if (d.moving == RT_STORED_FORM) { // stored (sin, cos)
+      o->sin_t = d.a.x;
+      o->cos_t = d.a.y;
+    } else {
+      double rad = d.s * PI / 180.0;
+      o->sin_t = std::sin(rad);
+      o->cos_t = std::cos(rad);
+    }
     Box bb = c->bbox;
     V mn = mk(INF, INF, INF), mx = mk(-INF, -INF, -INF);
     for (int i = 0; i < 2; i++)

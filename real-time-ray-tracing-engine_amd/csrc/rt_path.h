@@ -304,9 +304,15 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
       c2 = t, k2 = cl;
     }
   };
+  Ray lr = r;
+  int lr_first = -1, lr_count = 0; // chain lr is in (boundary items often share one)
   for (int k = 0; k < M.b_count; ++k) {
     const DItem it = S.bitems[M.b_first + k];
-    Ray lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
+    if (it.xf_first != lr_first || it.xf_count != lr_count) {
+      lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
+      lr_first = it.xf_first;
+      lr_count = it.xf_count;
+    }
     if (it.kind == I_SPHERE) { // sphere_root's two roots
       const DSphere &sp = S.spheres[it.idx];
       V3 cc = v3(sp.c0[0] + lr.tm * sp.dir[0], sp.c0[1] + lr.tm * sp.dir[1],

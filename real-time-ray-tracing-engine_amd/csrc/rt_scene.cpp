@@ -21,6 +21,7 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <map>
 
 namespace rtx {
 namespace {
@@ -153,7 +154,7 @@ struct Compiler {
       P3 rv{x.s, x.s, x.s};
       P3 c0 = p3(x.a);
       if (x.moving) { // Sphere.cpp:15-23
-        P3 dir = sub(p3(x.b), c0);
+        P3 dir = sphere_dir(x);
         P3 a0 = add(c0, scl(0, dir)), a1 = add(c0, scl(1, dir));
         b = bx_join(bx_points(sub(a0, rv), add(a0, rv)), bx_points(sub(a1, rv), add(a1, rv)));
       } else {
@@ -180,8 +181,8 @@ struct Compiler {
     }
     case RT_OBJ_ROTATE_Y: { // RotateY.cpp:5-35
       if (!visit(x.child)) return false;
-      double rad = x.s * kPi / 180.0;
-      double s = std::sin(rad), c = std::cos(rad);
+      double s, c;
+      rot_sincos(x, s, c);
       const Bx &cb = box[x.child];
       double mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
       for (int i = 0; i < 2; i++)
@@ -292,12 +293,30 @@ struct Compiler {
     return fail("unknown object kind");
   }
 
+  // Sphere displacement c1 - c0 (Sphere.cpp:15-23: m_center = Ray(c0, c1 - c0));
+  // moving == RT_STORED_FORM hands over the stored displacement itself.
+  static P3 sphere_dir(const rt_object_desc &x) {
+    if (x.moving == RT_STORED_FORM) return p3(x.b);
+    return x.moving ? sub(p3(x.b), p3(x.a)) : P3{0, 0, 0};
+  }
+  // RotateY's (sin, cos) (RotateY.cpp:7-9), or the stored pair.
+  static void rot_sincos(const rt_object_desc &x, double &s, double &c) {
+    if (x.moving == RT_STORED_FORM) {
+      s = x.a.x;
+      c = x.a.y;
+      return;
+    }
+    double rad = x.s * kPi / 180.0;
+    s = std::sin(rad);
+    c = std::cos(rad);
+  }
+
   int sphere_record(int o) {
     if (sphere_of[o] >= 0) return sphere_of[o];
     const rt_object_desc &x = D->objects[o];
     DSphere s;
     P3 c0 = p3(x.a);
-    P3 dir = x.moving ? sub(p3(x.b), c0) : P3{0, 0, 0}; // Sphere.cpp:15-23: m_center = Ray(c0, c1-c0)
+    P3 dir = sphere_dir(x);
     s.c0[0] = c0.x, s.c0[1] = c0.y, s.c0[2] = c0.z;
     s.dir[0] = dir.x, s.dir[1] = dir.y, s.dir[2] = dir.z;
     s.r = std::fmax(0, x.s);
@@ -334,8 +353,13 @@ struct Compiler {
     return quad_of[o];
   }
 
+  std::map<std::vector<int>, int> chain_first; // identical chains share their xforms
   int emit_chain(const std::vector<int> &chain) {
+    if (chain.empty()) return 0;
+    auto known = chain_first.find(chain);
+    if (known != chain_first.end()) return known->second;
     int first = (int)H.xforms.size();
+    chain_first[chain] = first;
     for (int o : chain) {
       const rt_object_desc &x = D->objects[o];
       DXform X;
@@ -346,10 +370,8 @@ struct Compiler {
         X.b = x.a.y;
         X.c = x.a.z;
       } else { // RotateY.cpp:7-9
-        double rad = x.s * kPi / 180.0;
         X.kind = X_ROTATE_Y;
-        X.a = std::sin(rad);
-        X.b = std::cos(rad);
+        rot_sincos(x, X.a, X.b);
       }
       H.xforms.push_back(X);
     }
@@ -358,9 +380,9 @@ struct Compiler {
 
   // Reference box rules for RotateY (RotateY.cpp:10-34) and Translate
   // (AABBUtility.hpp:7-11), applied innermost transform first.
-  Bx rot_box(const Bx &cb, double angle) {
-    double rad = angle * kPi / 180.0;
-    double s = std::sin(rad), c = std::cos(rad);
+  Bx rot_box(const Bx &cb, const rt_object_desc &x) {
+    double s, c;
+    rot_sincos(x, s, c);
     double mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
     for (int i = 0; i < 2; i++)
       for (int j = 0; j < 2; j++)
@@ -389,7 +411,7 @@ struct Compiler {
   Bx chain_box(Bx b, const std::vector<int> &chain) {
     for (size_t k = chain.size(); k-- > 0;) {
       const rt_object_desc &x = D->objects[chain[k]];
-      b = (x.kind == RT_OBJ_ROTATE_Y) ? rot_box(b, x.s) : trans_box(b, x.a);
+      b = (x.kind == RT_OBJ_ROTATE_Y) ? rot_box(b, x) : trans_box(b, x.a);
     }
     return b;
   }

@@ -14,6 +14,7 @@ RT_ERR_UNSUPPORTED = -4
 RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_NOISE = 0, 1, 2
 RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT_ISOTROPIC = range(5)
 RT_OBJ_SPHERE, RT_OBJ_QUAD, RT_OBJ_LIST, RT_OBJ_ROTATE_Y, RT_OBJ_TRANSLATE, RT_OBJ_MEDIUM = range(6)
+RT_STORED_FORM = 2  # rt_object_desc.moving: sphere displacement / rotate_y (sin, cos) as stored
 RT_OUT_SCALED, RT_OUT_SUM = 0, 1
 RT_PERLIN_POINTS = 256
 
