@@ -47,16 +47,17 @@ def dist_env():
 
 def algorithmic_bytes(st, info, n_pixels):
     """Bytes the kernel must fetch/store per launch under the device layout
-    (SURVEY §8d formula): node fetches x node size + primitive tests x (leaf ref
-    + item + primitive record) + light-pdf primitive tests + material/texture per
+    (SURVEY §8d formula): node fetches x node size + primitive tests x (item +
+    primitive record) + medium tests x (item + medium + boundary records) +
+    light-pdf primitive tests x (light leaf + record) + material/texture per
     shading event + the fp64 accumulator store per pixel."""
-    item, ref, light_leaf, mat_tex = 32, 4, 48, 96
+    item, light_leaf, mat_tex = 32, 48, 96
     b = st["node_visits"] * info["node_bytes"]
-    b += st["sphere_tests"] * (ref + item + info["sphere_bytes"])
-    b += st["quad_tests"] * (ref + item + info["quad_bytes"])
-    b += st["other_tests"] * (ref + item + 1024)  # medium: record + boundary items
+    b += st["sphere_tests"] * (item + info["sphere_bytes"])
+    b += st["quad_tests"] * (item + info["quad_bytes"])
+    b += st["other_tests"] * (item + 1024)  # medium: record + boundary items
     b += st["light_tests"] * (light_leaf + info["quad_bytes"])
-    b += (st["segments"]) * mat_tex
+    b += st["shade_events"] * mat_tex
     b += n_pixels * 24
     return b
 
@@ -64,11 +65,12 @@ def algorithmic_bytes(st, info, n_pixels):
 def cpu_baseline(scene, cam_full, threads):
     """The reference's own C++ path (oracle/_ref, built from /root/reference/src)
     with its -p decomposition over `threads` host threads, on a bounded sample:
-    the full frame at 2x2 strata (same scene, depth, resolution)."""
+    the full frame at 4x4 strata (same scene, depth, resolution; ~10 s)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     from rtx.scene import camera_desc  # noqa: F401
-    cam = scene.camera_desc(image_width=cam_full.image_width, samples_per_pixel=4,
+    spp = 16
+    cam = scene.camera_desc(image_width=cam_full.image_width, samples_per_pixel=spp,
                             max_depth=cam_full.max_depth)
     if O.ref_available():
         t = time.time()
@@ -79,11 +81,11 @@ def cpu_baseline(scene, cam_full, threads):
         t = time.time()
         O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=threads)
         dt = time.time() - t
-        n = cam.image_width * max(1, int(cam.image_width / cam.aspect_ratio)) * 4
+        n = cam.image_width * max(1, int(cam.image_width / cam.aspect_ratio)) * spp
         kind = "port"
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": kind,
-            "sample": "%dx%d @ 4 spp (2x2 strata), depth %d, %s, %.1f s" % (
-                cam.image_width, max(1, int(cam.image_width / cam.aspect_ratio)),
+            "sample": "%dx%d @ %d spp, depth %d, %s, %.1f s" % (
+                cam.image_width, max(1, int(cam.image_width / cam.aspect_ratio)), spp,
                 cam.max_depth, scene_name_of(scene), dt)}
 
 
@@ -219,6 +221,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": traffic, "kernel_ms": round(avg_ms, 3),
+                     "note": "achieved = SURVEY 8d algorithmic bytes / kernel time; the scene "
+                             "is L1/L2-resident, so it can exceed HBM peak; traffic = PMC "
+                             "FETCH_SIZE x2 + WRITE_SIZE per launch (the accumulator)",
                      "bytes_per_launch": int(bytes_launch),
                      "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
                      "counters": st},
