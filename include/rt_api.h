@@ -224,7 +224,7 @@ typedef struct rt_scene_info {
   int32_t quad_bytes;   /* bytes per quad record */
   int64_t device_bytes; /* total device bytes of the scene */
   int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise */
-  int32_t _pad;
+  int32_t lds_nodes;    /* BVH nodes (BFS prefix) the kernel stages in LDS per block */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

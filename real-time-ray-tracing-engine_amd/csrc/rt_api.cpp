@@ -22,6 +22,7 @@
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
+extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes);
 extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double scale,
                                           uint8_t *bytes, hipStream_t stream);
 
@@ -244,6 +245,20 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
   if (const char *fx = std::getenv("RTX_EXTRA_FEATURES")) // debug: widen the instance
     d.features |= std::atoi(fx) & 15;
+  // traversal stack: one entry per BVH level suffices (a pushed entry is the
+  // sibling of a node on the current root path); LDS prefix of the BFS-ordered
+  // nodes sized to what the instance's occupancy leaves free
+  d.stack_depth = std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
+  {
+    int budget = 0;
+    hipError_t be = rtk_node_budget(d.features, d.stack_depth, &budget);
+    if (be != hipSuccess) {
+      rt_scene_destroy(s);
+      return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
+    }
+    if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
+    d.n_lds_nodes = std::max(0, std::min(budget, (int32_t)H.nodes.size()));
+  }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
 
   rt_scene_info &in = s->info;
@@ -260,6 +275,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.quad_bytes = (int32_t)sizeof(DQuad);
   in.device_bytes = (int64_t)off;
   in.features = d.features;
+  in.lds_nodes = d.n_lds_nodes;
   *out = s;
   return RT_OK;
 }

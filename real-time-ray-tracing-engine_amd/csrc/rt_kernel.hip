@@ -44,17 +44,29 @@ constexpr int kWaves = 4; // waves (tiles) per 256-thread block
 template <bool STATS, unsigned F>
 __global__ __launch_bounds__(256) RT_OCCUPANCY void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
-  __shared__ int stack_lds[kWaves][RT_STACK_DEPTH][64];
+  // dynamic LDS: traversal stacks [kWaves][S.stack_depth][64] ints, then the
+  // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
+  extern __shared__ int4 dyn_lds[];
   __shared__ double acc_lds[kWaves][64][3];
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  int *stack_base = reinterpret_cast<int *>(dyn_lds);
+  DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + kWaves * S.stack_depth * 64);
+  const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g;
+  if (S.n_lds_nodes > 0) { // stage the top of the BVH (BFS prefix) once per block
+    const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
+    int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
+    const int n16 = S.n_lds_nodes * (int)(sizeof(DNode) / 16);
+    for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+  }
   const int tile = blockIdx.x * kWaves + wv;
   const int n_tiles = P.tiles_x * P.tiles_y;
   if (tile >= n_tiles) return; // whole wave exits together
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
   const int x0 = tx * 8, y0 = P.row_begin + ty * 8;
-  int *stk = &stack_lds[wv][0][lane];
+  int *stk = stack_base + wv * S.stack_depth * 64 + lane;
   double *acc = &acc_lds[wv][0][0];
   acc[lane * 3 + 0] = 0.0;
   acc[lane * 3 + 1] = 0.0;
@@ -97,7 +109,7 @@ __global__ __launch_bounds__(256) RT_OCCUPANCY void render_tiles(DScene S, DCame
     if (__ballot(ps.active) == 0) break;
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS, F>(S, C, ps, key, stk, cnt);
+      bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.L.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.L.y);
@@ -174,6 +186,28 @@ const RenderFn *render_table(bool stats) {
 } // namespace
 
 // ---------------------------------------------------------------- launchers
+extern "C" size_t rtk_lds_bytes(int stack_depth, int n_lds_nodes) {
+  return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * sizeof(DNode);
+}
+
+// LDS bytes per block left for the staged BVH prefix at the occupancy the
+// instance's register count allows (blocks of kWaves waves, one per SIMD).
+extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes) {
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(render_table(false)[features & F_ALL]));
+  if (e != hipSuccess) return e;
+  const int regs = ((a.numRegs + 7) / 8) * 8;
+  int waves_per_simd = regs > 0 ? 512 / regs : 8;
+  if (waves_per_simd > 8) waves_per_simd = 8;
+  if (waves_per_simd < 1) waves_per_simd = 1;
+  const size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
+  size_t per_block = lds_cu / waves_per_simd;
+  if (per_block > cap) per_block = cap;
+  size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(stack_depth, 0);
+  *n_nodes = per_block > fixed ? (int)((per_block - fixed) / sizeof(DNode)) : 0;
+  return hipSuccess;
+}
+
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
@@ -181,7 +215,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   int blocks = (n_tiles + kWaves - 1) / kWaves;
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), 0, stream, *S, *C, *P, out, stats);
+  size_t lds = rtk_lds_bytes(S->stack_depth, S->n_lds_nodes);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, *P, out, stats);
   return hipGetLastError();
 }
 

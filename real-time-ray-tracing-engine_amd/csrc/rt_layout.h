@@ -129,6 +129,8 @@ struct DScene {      // kernel argument (by value)
   int32_t n_root_items;
   int32_t features;      // RT_FEAT_* bits: selects the specialised kernel instance
   int32_t n_mitems;
+  int32_t stack_depth;   // per-lane traversal stack entries (BVH depth + 1)
+  int32_t n_lds_nodes;   // nodes [0, n_lds_nodes) are staged in LDS (BFS order: top levels)
 };
 
 // Scene features (kernel specialisation keys)

@@ -22,6 +22,11 @@
 #define RT_HD
 #define RT_FI inline
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_LDS __attribute__((address_space(3))) // LDS pointer: ds_read, not flat loads
+#else
+#define RT_LDS
+#endif
 
 namespace rtp {
 
@@ -459,9 +464,12 @@ struct Counters {
 
 // Closest hit over the world BVH.  Primitive items record only (t, item) during
 // traversal and build the hit record once at the end; media build theirs when hit.
+// `lnodes` is the LDS copy of nodes [0, S.n_lds_nodes) (the host emulator passes
+// S.nodes itself).
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
-                                      uint32_t bounce, int *stk, Counters &cnt) {
+                                      uint32_t bounce, int *stk, const RT_LDS DNode *lnodes,
+                                      Counters &cnt) {
   const double tmin = 0.001; // Camera.cpp:242
   double closest = kInf;
   int best = -1;
@@ -497,14 +505,28 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       }
       // ---- inner node: test both children's boxes
       if (STATS) cnt.nodes++;
-      const DNode &N = S.nodes[cur];
+      DNode N;
+      if (cur < S.n_lds_nodes) {
+        const RT_LDS DNode &L = lnodes[cur];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          N.lo0[k] = L.lo0[k];
+          N.hi0[k] = L.hi0[k];
+          N.lo1[k] = L.lo1[k];
+          N.hi1[k] = L.hi1[k];
+        }
+        N.entry[0] = L.entry[0];
+        N.entry[1] = L.entry[1];
+      } else {
+        N = S.nodes[cur];
+      }
       const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
       const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
       const int e0 = N.entry[0], e1 = N.entry[1];
       const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
       if (h0 && h1) {
         bool first0 = tn0 <= tn1;
-        if (sp < RT_STACK_DEPTH) stk[64 * sp++] = first0 ? e1 : e0;
+        if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
         cur = first0 ? e0 : e1;
       } else if (h0) {
         cur = e0;
@@ -690,10 +712,11 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 // when the path ends (its radiance is then final in ps.L).
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
-                                        const Key &key, int *stk, Counters &cnt) {
+                                        const Key &key, int *stk, const RT_LDS DNode *lnodes,
+                                        Counters &cnt) {
   const uint32_t b = ps.bounce;
   Hit h;
-  if (!trace<STATS, F>(S, ps.ray, h, key, b, stk, cnt)) {
+  if (!trace<STATS, F>(S, ps.ray, h, key, b, stk, lnodes, cnt)) {
     ps.L = ps.L + ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
     return false;
   }

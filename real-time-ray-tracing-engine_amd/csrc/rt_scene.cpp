@@ -652,17 +652,18 @@ struct Compiler {
       H.n_root_items = bn[root].count;
       return;
     }
-    // flatten: DFS over inner build nodes; each DNode holds both children's boxes
+    // flatten in BFS order (the top levels come first: they are the nodes every
+    // ray visits, and the kernel stages a prefix of the array in LDS); each DNode
+    // holds both children's boxes
     std::vector<int> map(bn.size(), -1);
     std::vector<int> order;
-    std::function<void(int)> dfs = [&](int b) {
-      if (bn[b].left < 0) return;
-      map[b] = (int)order.size();
-      order.push_back(b);
-      dfs(bn[b].left);
-      dfs(bn[b].right);
-    };
-    dfs(root);
+    order.push_back(root);
+    for (size_t q = 0; q < order.size(); ++q) {
+      const BNode &p = bn[order[q]];
+      map[order[q]] = (int)q;
+      if (bn[p.left].left >= 0) order.push_back(p.left);
+      if (bn[p.right].left >= 0) order.push_back(p.right);
+    }
     H.nodes.resize(order.size());
     for (size_t i = 0; i < order.size(); ++i) {
       const BNode &p = bn[order[i]];

@@ -98,7 +98,7 @@ class SceneInfo(C.Structure):
                 ("n_objects", C.c_int32), ("n_light_leaves", C.c_int32),
                 ("bvh_depth", C.c_int32), ("node_bytes", C.c_int32),
                 ("sphere_bytes", C.c_int32), ("quad_bytes", C.c_int32),
-                ("device_bytes", C.c_int64), ("features", C.c_int32), ("_pad", C.c_int32)]
+                ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).
