@@ -35,14 +35,19 @@ namespace {
 using namespace rtp;
 constexpr int kWaves = 4; // waves (tiles) per 256-thread block
 
-#ifdef RT_WAVES_PER_EU
-#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
-#else
-#define RT_OCCUPANCY
+// Occupancy target per instance (waves per SIMD): the compiler may spill a few
+// registers to reach it.  Measured: 4 for the plain instance (C3
+// +12 % over 3), 3 for the rich ones (C4 +8.6 % over the 2 that 224 VGPRs give).
+#ifndef RT_WAVES_F0
+#define RT_WAVES_F0 4
 #endif
+#ifndef RT_WAVES_OTHER
+#define RT_WAVES_OTHER 3
+#endif
+#define RT_WAVES_PER_EU(F) ((F) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER)
 
 template <bool STATS, unsigned F>
-__global__ __launch_bounds__(256) RT_OCCUPANCY void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   // dynamic LDS: traversal stacks [kWaves][S.stack_depth][64] ints, then the
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
