@@ -104,7 +104,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
           key.sample = (uint32_t)ps.sample;
           ps.ray = camera_ray(C, key, i, j, ps.sample);
           ps.T = v3(1.0, 1.0, 1.0);
-          ps.L = v3(0.0, 0.0, 0.0);
           ps.bounce = 0;
           ps.active = C.max_depth > 0;
           if (STATS) n_samples++;
@@ -116,9 +115,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
       if (STATS) n_segments++;
       bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt);
       if (!cont) {
-        atomicAdd(&acc[ps.slot * 3 + 0], ps.L.x);
-        atomicAdd(&acc[ps.slot * 3 + 1], ps.L.y);
-        atomicAdd(&acc[ps.slot * 3 + 2], ps.L.z);
+        atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
+        atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
+        atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
         ps.active = false;
       }
     }

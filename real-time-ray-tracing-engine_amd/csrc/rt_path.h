@@ -689,8 +689,7 @@ RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double 
 // ------------------------------------------------------------ integrator
 struct PathState {
   Ray ray;
-  V3 T; // throughput
-  V3 L; // radiance gathered so far
+  V3 T; // throughput; when the path ends: its radiance (T x terminal value)
   uint32_t bounce;
   int slot;   // tile pixel slot 0..63
   int sample; // linear stratum index
@@ -702,14 +701,16 @@ struct PathState {
 RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
   ps.bounce++;
   if ((int)ps.bounce >= C.max_depth) {
-    ps.L = ps.L + ps.T * v3(0.0, 0.0, 0.0);
+    ps.T = ps.T * v3(0.0, 0.0, 0.0);
     return false;
   }
   return true;
 }
 
 // One segment of Camera::ray_color in forward (throughput) form.  Returns false
-// when the path ends (its radiance is then final in ps.L).
+// when the path ends; its radiance is then in ps.T.  The recursion's
+// L = e + a*L' sums emission only where a path ends (lights never scatter), so the
+// forward form needs no radiance register: the terminal T x value is the sample.
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
                                         const Key &key, int *stk, const RT_LDS DNode *lnodes,
@@ -717,7 +718,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   const uint32_t b = ps.bounce;
   Hit h;
   if (!trace<STATS, F>(S, ps.ray, h, key, b, stk, lnodes, cnt)) {
-    ps.L = ps.L + ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
+    ps.T = ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
     return false;
   }
   const DMat M = S.mats[h.mat];
@@ -726,7 +727,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     // Always add T * emitted (0 on the back face): a NaN/inf throughput must
     // poison the sample as the reference recursion does (NaN * 0 = NaN).
     V3 e = h.front ? tex_value<F>(S, M.tex, h.p) : v3(0.0, 0.0, 0.0);
-    ps.L = ps.L + ps.T * e;
+    ps.T = ps.T * e;
     return false;
   }
   double e0, e1, d0, d1;
@@ -822,7 +823,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     spdf = 1 / (4 * kPi);
   }
   if (spdf == 0.0 && pdf > 0.0 && pdf < kInf) { // zero-weight continuation
-    ps.L = ps.L + ps.T * v3(0.0, 0.0, 0.0);      // (keeps an earlier NaN/inf alive)
+    ps.T = ps.T * v3(0.0, 0.0, 0.0);             // (keeps an earlier NaN/inf alive)
     return false;
   }
   V3 wgt = (1 / pdf) * (spdf * att);

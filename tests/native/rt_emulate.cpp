@@ -28,15 +28,14 @@ void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, i
     PathState ps;
     ps.ray = camera_ray(C, key, i, j, k);
     ps.T = v3(1.0, 1.0, 1.0);
-    ps.L = v3(0.0, 0.0, 0.0);
     ps.bounce = 0;
     ps.active = C.max_depth > 0;
     while (ps.active) {
       bool cont = segment<false, F>(S, C, ps, key, stk, S.nodes, cnt);
       if (!cont) {
-        acc[0] += ps.L.x;
-        acc[1] += ps.L.y;
-        acc[2] += ps.L.z;
+        acc[0] += ps.T.x;
+        acc[1] += ps.T.y;
+        acc[2] += ps.T.z;
         ps.active = false;
       }
     }
