@@ -277,6 +277,10 @@ private:
     if (ty == "sphere") {
       if (need_material && no_mat) throw SceneError("world sphere without material");
       int m = mat(mref);
+      if (o.has("displacement")) // stored form: Sphere's m_center direction (c1 - c0)
+        return add_object(RT_OBJ_SPHERE, m, -1, 0, v3(o.at("center"), "center"),
+                          v3(o.at("displacement"), "displacement"), z, o.at("radius").number(),
+                          RT_STORED_FORM, -1);
       if (o.has("center2"))
         return add_object(RT_OBJ_SPHERE, m, -1, 0, v3(o.at("center"), "center"),
                           v3(o.at("center2"), "center2"), z, o.at("radius").number(), 1, -1);
@@ -313,6 +317,12 @@ private:
     }
     if (ty == "rotate_y") {
       int ch = object(o.at("object"), need_material);
+      if (o.has("sin_cos")) { // stored form: RotateY's (sin, cos)
+        const Value &sc = o.at("sin_cos");
+        if (!sc.is_array() || sc.arr.size() != 2) throw SceneError("rotate_y.sin_cos must be [sin, cos]");
+        return add_object(RT_OBJ_ROTATE_Y, -1, ch, 0, rt_vec3{sc.arr[0].number(), sc.arr[1].number(), 0.0},
+                          z, z, 0.0, RT_STORED_FORM, -1);
+      }
       return add_object(RT_OBJ_ROTATE_Y, -1, ch, 0, z, z, z, o.at("angle").number(), 0, -1);
     }
     if (ty == "translate") {

@@ -255,6 +255,10 @@ def load_scene(src):
             if need_material and mref is None:
                 raise SceneError("world sphere without material")
             m = mat(mref)
+            if "displacement" in o:  # stored form: Sphere's m_center direction (c1 - c0)
+                return S.add_object(abi.RT_OBJ_SPHERE, material=m, a=_v3(o["center"]),
+                                    b=_v3(o["displacement"]), s=float(o["radius"]),
+                                    moving=abi.RT_STORED_FORM)
             if "center2" in o:
                 return S.add_object(abi.RT_OBJ_SPHERE, material=m, a=_v3(o["center"]),
                                     b=_v3(o["center2"]), s=float(o["radius"]), moving=1)
@@ -277,6 +281,13 @@ def load_scene(src):
             return S.add_list(ids)
         if ty == "rotate_y":
             ch = obj(o["object"], need_material)
+            if "sin_cos" in o:  # stored form: RotateY's (sin, cos)
+                sc = o["sin_cos"]
+                if len(sc) != 2:
+                    raise SceneError("rotate_y.sin_cos must be [sin, cos]")
+                return S.add_object(abi.RT_OBJ_ROTATE_Y, child=ch,
+                                    a=[float(sc[0]), float(sc[1]), 0.0],
+                                    moving=abi.RT_STORED_FORM)
             return S.add_object(abi.RT_OBJ_ROTATE_Y, child=ch, s=float(o["angle"]))
         if ty == "translate":
             ch = obj(o["object"], need_material)
@@ -299,6 +310,87 @@ def load_scene(src):
         light_ids = [obj(o, need_material=False) for o in doc["lights"]]
         S.lights = S.add_list(light_ids)
     return S
+
+
+def dump_scene(S):
+    """SceneDescription -> JSON document (dict) that load_scene reads back into
+    the same tables: every texture/material/Perlin table is named by its index
+    and referenced by name, objects keep their nesting (so the lazy loader
+    re-creates every table entry and object in the same order), boxes come back
+    as their 6-quad lists, and the stored forms (sphere displacement, rotate_y
+    sin/cos) are written as such, so no double changes."""
+    v = lambda x: [x.x, x.y, x.z]  # noqa: E731
+    doc = {}
+    if S.camera:
+        doc["camera"] = copy.deepcopy(S.camera)
+    doc["use_bvh"] = bool(S.use_bvh)
+    if S.perlin:
+        doc["perlin"] = {"p%d" % i: {"rand_vec": [v(p.rand_vec[k]) for k in range(256)],
+                                     "perm_x": list(p.perm_x), "perm_y": list(p.perm_y),
+                                     "perm_z": list(p.perm_z)}
+                         for i, p in enumerate(S.perlin)}
+    tex = {}
+    for i, t in enumerate(S.textures):
+        if t.kind == abi.RT_TEX_SOLID:
+            tex["t%d" % i] = {"type": "solid", "color": v(t.color)}
+        elif t.kind == abi.RT_TEX_CHECKER:
+            tex["t%d" % i] = {"type": "checker", "scale": t.scale,
+                              "even": "t%d" % t.even, "odd": "t%d" % t.odd}
+        else:
+            tex["t%d" % i] = {"type": "noise", "scale": t.scale, "perlin": "p%d" % t.perlin}
+    if tex:
+        doc["textures"] = tex
+    mats = {}
+    for i, m in enumerate(S.materials):
+        if m.kind == abi.RT_MAT_LAMBERTIAN:
+            mats["m%d" % i] = {"type": "lambertian", "texture": "t%d" % m.texture}
+        elif m.kind == abi.RT_MAT_METAL:
+            mats["m%d" % i] = {"type": "metal", "albedo": v(m.albedo), "fuzz": m.fuzz}
+        elif m.kind == abi.RT_MAT_DIELECTRIC:
+            mats["m%d" % i] = {"type": "dielectric", "refraction_index": m.refraction_index}
+        elif m.kind == abi.RT_MAT_DIFFUSE_LIGHT:
+            mats["m%d" % i] = {"type": "diffuse_light", "texture": "t%d" % m.texture}
+        else:
+            mats["m%d" % i] = {"type": "isotropic", "texture": "t%d" % m.texture}
+    if mats:
+        doc["materials"] = mats
+
+    def obj(i):
+        o = S.objects[i]
+        mref = ("m%d" % o.material) if o.material >= 0 else None
+        if o.kind == abi.RT_OBJ_SPHERE:
+            d = {"type": "sphere", "center": v(o.a), "radius": o.s}
+            if o.moving == abi.RT_STORED_FORM:
+                d["displacement"] = v(o.b)
+            elif o.moving:
+                d["center2"] = v(o.b)
+        elif o.kind == abi.RT_OBJ_QUAD:
+            d = {"type": "quad", "Q": v(o.a), "u": v(o.b), "v": v(o.c)}
+        elif o.kind == abi.RT_OBJ_LIST:
+            return {"type": "list",
+                    "objects": [obj(S.children[o.child + k]) for k in range(o.count)]}
+        elif o.kind == abi.RT_OBJ_ROTATE_Y:
+            d = {"type": "rotate_y", "object": obj(o.child)}
+            if o.moving == abi.RT_STORED_FORM:
+                d["sin_cos"] = [o.a.x, o.a.y]
+            else:
+                d["angle"] = o.s
+            return d
+        elif o.kind == abi.RT_OBJ_TRANSLATE:
+            return {"type": "translate", "offset": v(o.a), "object": obj(o.child)}
+        else:
+            return {"type": "constant_medium", "boundary": obj(o.child), "density": o.s,
+                    "phase": "m%d" % o.phase}
+        if mref is not None:
+            d["material"] = mref
+        return d
+
+    w = S.objects[S.world]
+    doc["world"] = [obj(S.children[w.child + k]) for k in range(w.count)]
+    if S.lights >= 0:
+        li = S.objects[S.lights]
+        doc["lights"] = [obj(S.children[li.child + k]) for k in range(li.count)]
+    return doc
 
 
 def dump_float(x):
