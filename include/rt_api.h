@@ -245,7 +245,8 @@ int rt_scene_destroy(rt_scene *scene);
 int rt_render(rt_scene *scene, const rt_frame *frame, const rt_render_params *params,
               double *host_rgb);
 
-/* Same work, asynchronously on `hip_stream` (NULL = the scene's own stream),
+/* Same work, asynchronously on `hip_stream` (NULL = the HIP null stream, so work
+   is ordered with a framework's default stream, e.g. torch's),
    writing/accumulating into a device buffer of W*(row_end-row_begin)*3 doubles. */
 int rt_render_device(rt_scene *scene, const rt_frame *frame,
                      const rt_render_params *params, double *device_rgb,

@@ -356,7 +356,7 @@ int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, 
   if (rc) return rc;
   if ((rc = to_launch(f, p, L))) return rc;
   DeviceGuard g(s->device);
-  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : s->stream;
+  hipStream_t st = (hipStream_t)hip_stream; // NULL = the HIP null stream (HIP convention)
   return launch(s, C, L, dev_rgb, nullptr, st);
 }
 

@@ -166,3 +166,22 @@ def test_errors_are_reported_not_fatal():
         with pytest.raises(RtError):
             R.render(f, seed=1, rows=(3, 2))
         R.render(f, seed=1)                       # still usable afterwards
+
+
+@pytest.mark.gpu
+def test_render_device_is_ordered_with_torch_stream():
+    """rt_render_device on the null stream is ordered with torch's default
+    stream: zero_, render, accumulate, .cpu() need no explicit synchronize."""
+    import torch
+    S = scene("cornell")
+    cam = S.camera_desc(image_width=48, samples_per_pixel=4, max_depth=6)
+    f = camera_frame(cam)
+    buf = torch.full((f.image_height, f.image_width, 3), 7.0, dtype=torch.float64, device="cuda")
+    with Renderer(S) as R:
+        for _ in range(3):
+            buf.zero_()
+            R.render_device(f, buf.data_ptr(), 0, seed=5, output=abi.RT_OUT_SUM, accumulate=1)
+            R.render_device(f, buf.data_ptr(), 0, seed=5, output=abi.RT_OUT_SUM, accumulate=1)
+            got = buf.cpu().numpy()  # syncs torch's stream only
+        one = R.render(f, seed=5, output=abi.RT_OUT_SUM)
+    np.testing.assert_allclose(got, 2 * one, rtol=1e-12, atol=1e-12)
