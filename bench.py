@@ -103,6 +103,14 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    # rehearsal of the N>1 path on one GPU: every rank on cuda:0, gloo all_reduce
+    # instead of RCCL reduce (the driver's 8-GPU runs use the defaults)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--share-device", action="store_true")
+    ap.add_argument("--shard", default="tiles", choices=["tiles", "strata"],
+                    help="N>1: tiles round-robin + gather (default) or strata + reduce")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0 compares the reduced frame with a 1-device render")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -113,11 +121,16 @@ def main():
 
     if ws != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
+    if args.share_device:
+        local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     name, width, spp, depth = CONFIGS[args.config]
     width = args.width or width
@@ -130,38 +143,75 @@ def main():
     n_strata = sq * sq
     s0 = rank * n_strata // ws
     s1 = (rank + 1) * n_strata // ws
+    tiles_mode = ws > 1 and args.shard == "tiles"
 
-    from rtx.dist import ShardedRenderer, max_over_ranks
+    from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks
     R = Renderer(scene, device=local)
     info = R.info()
-    stream = torch.cuda.current_stream(dev)
-    # two accumulators: the RCCL reduce of frame k overlaps the render of k+1
-    accs = [torch.zeros((H, W, 3), dtype=torch.float64, device=dev) for _ in range(2)]
-    pending = [None, None]
+    stream = torch.cuda.current_stream(dev)  # the null stream: ordered with RCCL's waits
 
     def render_fn(fr, acc, seed, strata):
-        # each rank overwrites its partial sums (no memset, no read-modify-write)
+        # overwrite the partial sums (no memset, no read-modify-write)
         R.render_device(fr, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=strata,
                         output=abi.RT_OUT_SUM, accumulate=0)
 
-    sharded = ShardedRenderer(render_fn, frame, rank, ws)
-    assert sharded.strata == (s0, s1)
+    def tile_render_fn(fr, buf, seed, tiles):
+        R.render_device(fr, buf.data_ptr(), stream.cuda_stream, seed=seed, samples=(0, -1),
+                        output=abi.RT_OUT_SUM, accumulate=0, tiles=tiles,
+                        layout=abi.RT_LAYOUT_TILES)
+
+    if tiles_mode:
+        shard = TileShardedRenderer(tile_render_fn, frame, rank, ws)
+        bufs = [shard.buffer(dev) for _ in range(2)]
+        gath = [shard.gather_buffer(dev) if rank == 0 else None for _ in range(2)]
+        launch_work = lambda seed, b: shard.render(bufs[b], seed)  # noqa: E731
+    else:
+        shard = ShardedRenderer(render_fn, frame, rank, ws)
+        assert shard.strata == (s0, s1)
+        bufs = [torch.zeros((H, W, 3), dtype=torch.float64, device=dev) for _ in range(2)]
+        launch_work = lambda seed, b: render_fn(frame, bufs[b], seed, (s0, s1 - s0))  # noqa: E731
+    final = {}      # rank 0: the last completed frame's raw sums, by step
+    inflight = []   # (step, buffer, work handle) in step order
     kernel_ms = []
+
+    def complete(k, b, work):
+        if work is not None:
+            work.wait()
+        if rank == 0:
+            if tiles_mode:
+                final["frame"] = shard.frame_sums(gath[b])  # reorder the gathered tiles
+            else:
+                final["frame"] = bufs[b]
+            final["step"] = k
+
+    def exchange(b):
+        if ws == 1:
+            return None
+        if tiles_mode:
+            if args.backend == "nccl":
+                return shard.gather(bufs[b], gath[b], async_op=True)
+            torch.cuda.synchronize(dev)  # gloo: host-staged, no CUDA gather
+            cpu = bufs[b].cpu()
+            parts = [torch.empty_like(cpu) for _ in range(ws)] if rank == 0 else None
+            dist.gather(cpu, gather_list=parts, dst=0)
+            if rank == 0:
+                gath[b].copy_(torch.stack(parts))
+            return None
+        if args.backend == "nccl":
+            return dist.reduce(bufs[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+        torch.cuda.synchronize(dev)  # gloo has no CUDA reduce
+        return dist.all_reduce(bufs[b], op=dist.ReduceOp.SUM, async_op=True)
 
     def step(k, seed):
         b = k % 2
-        if pending[b] is not None:  # buffer still being reduced from step k-2
-            pending[b].wait()
-            pending[b] = None
-        render_fn(frame, accs[b], seed, (s0, s1 - s0))
-        if ws > 1:
-            pending[b] = dist.reduce(accs[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+        while inflight and inflight[0][1] == b:  # this buffer's exchange (step k-2) first
+            complete(*inflight.pop(0))
+        launch_work(seed, b)
+        inflight.append((k, b, exchange(b)))
 
     def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        while inflight:
+            complete(*inflight.pop(0))
 
     for w in range(args.warmup):
         step(w, 1000 + w)
@@ -181,17 +231,32 @@ def main():
     if ws > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    check = None
+    if args.check and rank == 0:  # the last timed frame on rank 0 vs one device, all strata
+        assert final["step"] == args.steps - 1
+        last = final["frame"].clone()
+        ref = torch.empty_like(last)
+        render_fn(frame, ref, args.steps - 1, (0, n_strata))
+        torch.cuda.synchronize(dev)
+        err = (last - ref).abs().max().item()
+        scale = max(1.0, ref.abs().max().item())
+        check = {"max_abs_diff": err, "ok": bool(err <= 1e-9 * scale)}
+
     if ws > 1:  # kernel time measured after the timed region (no sync inside it)
         for k in range(min(2, args.steps)):
-            render_fn(frame, accs[0], 5000 + k, (s0, s1 - s0))
+            launch_work(5000 + k, 0)
             kernel_ms.append(R.last_kernel_ms())
 
     samples_per_step = W * H * n_strata  # whole frame, all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
     # roofline of the dominant (render) kernel on this rank, one launch
-    st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
-    bytes_launch = algorithmic_bytes(st, info, W * H)
+    if tiles_mode:
+        st = R.stats(frame, seed=0, tiles=(rank, ws), layout=abi.RT_LAYOUT_TILES)
+    else:
+        st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
+    px_launch = shard.tiles_per_rank * 64 if tiles_mode else W * H
+    bytes_launch = algorithmic_bytes(st, info, px_launch)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
@@ -217,7 +282,12 @@ def main():
         "data": "synthetic: JSON scene %s, seeded Philox sample stream" % name,
         "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
                    "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
-                   "parallelism": "stratum-shard x%d + RCCL reduce(sum)" % ws if ws > 1 else "1 GPU"},
+                   "parallelism": ("1 GPU" if ws == 1 else
+                                   "tile-shard x%d (tile t on rank t %% %d) + %s gather" % (
+                                       ws, ws, "RCCL" if args.backend == "nccl" else "gloo")
+                                   if tiles_mode else
+                                   "stratum-shard x%d + %s reduce(sum)" % (
+                                       ws, "RCCL" if args.backend == "nccl" else "gloo"))},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": traffic, "kernel_ms": round(avg_ms, 3),
@@ -228,6 +298,8 @@ def main():
                      "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
                      "counters": st},
     }
+    if check is not None:
+        out["check"] = check
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, cam, min(args.cpu_threads, os.cpu_count() or 1))
     if rank == 0:

@@ -192,6 +192,11 @@ enum {
   RT_OUT_SUM = 1     /* out = raw sum over the launched samples */
 };
 
+enum {
+  RT_LAYOUT_FRAME = 0,
+  RT_LAYOUT_TILES = 1
+};
+
 typedef struct rt_render_params {
   int32_t row_begin;    /* first image row (inclusive) — StaticCamera.cpp:235 batches */
   int32_t row_end;      /* last row (exclusive); 0,0 = whole image */
@@ -200,6 +205,16 @@ typedef struct rt_render_params {
   uint64_t seed;        /* RNG key; replaces curand_init(time(nullptr)+pixel) */
   int32_t output;       /* RT_OUT_SCALED / RT_OUT_SUM */
   int32_t accumulate;   /* rt_render_device only: 1 = add into the buffer, 0 = overwrite */
+  /* Tile subset (multi-GPU tile sharding): the 8x8 tiles of the row range, in
+     row-major tile order, are rendered for t = tile_first + k*tile_stride only.
+     tile_stride 0 or 1 with tile_first 0 = every tile. */
+  int32_t tile_first;
+  int32_t tile_stride;
+  int32_t layout;       /* RT_LAYOUT_FRAME: row-major pixels (index (j-row_begin)*W+i);
+                           RT_LAYOUT_TILES: the k-th rendered tile's 64 pixels at
+                           [k*64, k*64+64), pixel (x,y) of the tile at k*64 + y*8 + x
+                           (slots outside the image hold 0) */
+  int32_t _pad;
 } rt_render_params;
 
 /* Per-launch traversal/shading counters (for algorithmic-bytes accounting). */

@@ -118,7 +118,23 @@ int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
   L.accumulate = p->accumulate ? 1 : 0;
   L.tiles_x = (f->image_width + 7) / 8;
   L.tiles_y = (r1 - r0 + 7) / 8;
+  int stride = p->tile_stride <= 0 ? 1 : p->tile_stride;
+  if (p->tile_first < 0 || p->tile_first >= stride)
+    return set_err(RT_ERR_INVALID, "tile_first must be in [0, tile_stride)");
+  if (p->layout != RT_LAYOUT_FRAME && p->layout != RT_LAYOUT_TILES)
+    return set_err(RT_ERR_INVALID, "unknown output layout");
+  const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
+  L.tile_first = p->tile_first;
+  L.tile_stride = stride;
+  L.n_local_tiles = (int32_t)(n_tiles > p->tile_first ? (n_tiles - p->tile_first + stride - 1) / stride : 0);
+  L.compact = p->layout == RT_LAYOUT_TILES;
   return RT_OK;
+}
+
+// doubles an output of this launch covers
+size_t out_doubles(const rt_frame *f, const DLaunch &L) {
+  if (L.compact) return (size_t)L.n_local_tiles * 64 * 3;
+  return (size_t)f->image_width * (L.row_end - L.row_begin) * 3;
 }
 
 } // namespace
@@ -336,7 +352,7 @@ int rt_render(rt_scene *s, const rt_frame *f, const rt_render_params *p, double 
   rt_render_params q = *p;
   q.accumulate = 0;
   L.accumulate = 0;
-  size_t n = (size_t)f->image_width * (L.row_end - L.row_begin) * 3;
+  size_t n = out_doubles(f, L);
   if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
   if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream))) return rc;
   hipError_t e = hipMemcpyAsync(host_rgb, s->out_buf, n * sizeof(double), hipMemcpyDeviceToHost,
@@ -370,7 +386,7 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   if ((rc = to_launch(f, p, L))) return rc;
   DeviceGuard g(s->device);
   L.accumulate = 0;
-  size_t n = (size_t)f->image_width * (L.row_end - L.row_begin) * 3;
+  size_t n = out_doubles(f, L);
   if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
   hipError_t e = hipMemsetAsync(s->stats, 0, 8 * sizeof(unsigned long long), s->stream);
   if (e != hipSuccess) return hip_err(e, "hipMemsetAsync stats");

@@ -66,9 +66,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
     for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
   }
-  const int tile = blockIdx.x * kWaves + wv;
-  const int n_tiles = P.tiles_x * P.tiles_y;
-  if (tile >= n_tiles) return; // whole wave exits together
+  const int local_tile = blockIdx.x * kWaves + wv;
+  if (local_tile >= P.n_local_tiles) return; // whole wave exits together
+  const int tile = P.tile_first + local_tile * P.tile_stride;
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
   const int x0 = tx * 8, y0 = P.row_begin + ty * 8;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
@@ -127,14 +127,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
   // ---- tile epilogue: one coalesced store per pixel
   {
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
-    if (i < C.W && j < P.row_end) {
+    if (P.compact || (i < C.W && j < P.row_end)) { // tile slots outside the image hold 0
       double sx = acc[lane * 3 + 0], sy = acc[lane * 3 + 1], sz = acc[lane * 3 + 2];
       if (P.output == RT_OUT_SCALED) {
         sx = C.scale * sx;
         sy = C.scale * sy;
         sz = C.scale * sz;
       }
-      double *o = out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
+      double *o = P.compact ? out + 3 * ((size_t)local_tile * 64 + lane)
+                            : out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
       if (P.accumulate) {
         o[0] += sx;
         o[1] += sy;
@@ -215,8 +216,7 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
-  int n_tiles = P->tiles_x * P->tiles_y;
-  int blocks = (n_tiles + kWaves - 1) / kWaves;
+  int blocks = (P->n_local_tiles + kWaves - 1) / kWaves;
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->stack_depth, S->n_lds_nodes);

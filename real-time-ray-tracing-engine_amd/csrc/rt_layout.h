@@ -152,6 +152,9 @@ struct DLaunch {
   uint32_t seed_lo, seed_hi;
   int32_t output, accumulate;
   int32_t tiles_x, tiles_y;
+  int32_t tile_first, tile_stride; // tiles rendered: tile_first + k * tile_stride
+  int32_t n_local_tiles;           // k in [0, n_local_tiles)
+  int32_t compact;                 // RT_LAYOUT_TILES output
 };
 
 #endif

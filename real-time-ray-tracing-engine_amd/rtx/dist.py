@@ -1,4 +1,17 @@
-"""Multi-GPU frame rendering: stratum sharding + one reduce of the accumulator.
+"""Multi-GPU frame rendering.
+
+Two decompositions of one frame over the ranks of the default process group:
+
+* tile sharding (default in bench.py): the frame's 8x8 tiles are dealt out
+  round-robin, tile t to rank t % world, so cheap (sky) and expensive tiles
+  spread evenly; each rank renders ALL strata of its tiles into a compact tile
+  buffer (RT_LAYOUT_TILES) and rank 0 gathers the buffers (1/world of the frame
+  from each rank, over all of rank 0's xGMI links at once) and reorders them.
+  Every pixel is computed by exactly one GPU, so the frame is the one-GPU frame
+  bit for bit.
+* stratum sharding (below): ranks split the strata and reduce(sum) full-frame
+  accumulators — the SURVEY §8(e) recommendation; it moves ~2x the frame per
+  rank through a ring and changes the fp64 summation order.
 
 The reference is single-GPU (no NCCL/MPI).  Here a frame's strata
 (the sqrt(spp) x sqrt(spp) grid of StaticCamera.cpp:74-76, linear index
@@ -49,6 +62,64 @@ class ShardedRenderer:
     def image(self, acc):
         """Scaled radiance on rank 0 (pixel_samples_scale * sum)."""
         return acc * self.frame.pixel_samples_scale
+
+
+def tile_counts(frame, world):
+    """(tiles in the frame, tiles per rank padded to the largest shard)."""
+    n = ((frame.image_width + 7) // 8) * ((frame.image_height + 7) // 8)
+    return n, (n + world - 1) // world
+
+
+def tiles_to_frame(gathered, width, height):
+    """Gathered compact tile buffers [world, T_r, 64, 3] (rank r holds tiles
+    r, r + world, r + 2*world, ... in RT_LAYOUT_TILES order) -> frame [H, W, 3]."""
+    world, t_r = gathered.shape[0], gathered.shape[1]
+    tx, ty = (width + 7) // 8, (height + 7) // 8
+    n = tx * ty
+    flat = gathered.transpose(0, 1).reshape(t_r * world, 64, gathered.shape[-1])[:n]
+    img = flat.reshape(ty, tx, 8, 8, -1).permute(0, 2, 1, 3, 4).reshape(ty * 8, tx * 8, -1)
+    return img[:height, :width]
+
+
+class TileShardedRenderer:
+    """Renders one frame per call with tile t on rank t % world.
+
+    render_fn(frame, buf, seed, tiles=(first, stride)) must overwrite `buf`
+    ([T_r, 64, 3] float64) with the raw sums of all strata of those tiles in
+    RT_LAYOUT_TILES order (Renderer.render_device with output=RT_OUT_SUM,
+    accumulate=0, layout=RT_LAYOUT_TILES)."""
+
+    def __init__(self, render_fn, frame, rank=0, world=1):
+        self.render_fn = render_fn
+        self.frame = frame
+        self.rank, self.world = rank, world
+        self.n_tiles, self.tiles_per_rank = tile_counts(frame, world)
+
+    def buffer(self, device=None):
+        return torch.zeros((self.tiles_per_rank, 64, 3), dtype=torch.float64, device=device)
+
+    def gather_buffer(self, device=None):
+        return torch.zeros((self.world, self.tiles_per_rank, 64, 3), dtype=torch.float64,
+                           device=device)
+
+    def render(self, buf, seed):
+        self.render_fn(self.frame, buf, seed, (self.rank, self.world))
+
+    def gather(self, buf, gathered=None, async_op=False):
+        """Collect every rank's tiles on rank 0 (gathered: [world, T_r, 64, 3])."""
+        if self.world == 1:
+            gathered[0].copy_(buf)
+            return None
+        parts = list(gathered.unbind(0)) if self.rank == 0 else None
+        return dist.gather(buf, gather_list=parts, dst=0, async_op=async_op)
+
+    def frame_sums(self, gathered):
+        return tiles_to_frame(gathered, self.frame.image_width, self.frame.image_height)
+
+    def step(self, buf, gathered, seed):
+        self.render(buf, seed)
+        self.gather(buf, gathered)
+        return self.frame_sums(gathered) if self.rank == 0 else None
 
 
 def max_over_ranks(value, device=None):

@@ -43,7 +43,7 @@ def test_struct_sizes_match_header_layout():
     assert C.sizeof(abi.MaterialDesc) == 48
     assert C.sizeof(abi.ObjectDesc) == 104
     assert C.sizeof(abi.CameraDesc) == 144
-    assert C.sizeof(abi.RenderParams) == 32
+    assert C.sizeof(abi.RenderParams) == 48
     assert C.sizeof(abi.PerlinDesc) == 256 * 24 + 3 * 256 * 4
 
 
