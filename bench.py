@@ -155,16 +155,19 @@ def main():
         R.render_device(fr, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=strata,
                         output=abi.RT_OUT_SUM, accumulate=0)
 
-    def tile_render_fn(fr, buf, seed, tiles):
+    def tile_render_fn(fr, buf, seed, tiles, chunks):
         R.render_device(fr, buf.data_ptr(), stream.cuda_stream, seed=seed, samples=(0, -1),
                         output=abi.RT_OUT_SUM, accumulate=0, tiles=tiles,
-                        layout=abi.RT_LAYOUT_TILES)
+                        layout=abi.RT_LAYOUT_TILES, chunks=chunks)
 
     if tiles_mode:
         shard = TileShardedRenderer(tile_render_fn, frame, rank, ws)
         bufs = [shard.buffer(dev) for _ in range(2)]
         gath = [shard.gather_buffer(dev) if rank == 0 else None for _ in range(2)]
-        launch_work = lambda seed, b: shard.render(bufs[b], seed)  # noqa: E731
+        tsum = [None, None]  # per-tile sums (chunk sum) of each buffer
+
+        def launch_work(seed, b):
+            tsum[b] = shard.render(bufs[b], seed)
     else:
         shard = ShardedRenderer(render_fn, frame, rank, ws)
         assert shard.strata == (s0, s1)
@@ -189,9 +192,9 @@ def main():
             return None
         if tiles_mode:
             if args.backend == "nccl":
-                return shard.gather(bufs[b], gath[b], async_op=True)
+                return shard.gather(tsum[b], gath[b], async_op=True)
             torch.cuda.synchronize(dev)  # gloo: host-staged, no CUDA gather
-            cpu = bufs[b].cpu()
+            cpu = tsum[b].cpu()
             parts = [torch.empty_like(cpu) for _ in range(ws)] if rank == 0 else None
             dist.gather(cpu, gather_list=parts, dst=0)
             if rank == 0:
@@ -252,10 +255,11 @@ def main():
 
     # roofline of the dominant (render) kernel on this rank, one launch
     if tiles_mode:
-        st = R.stats(frame, seed=0, tiles=(rank, ws), layout=abi.RT_LAYOUT_TILES)
+        st = R.stats(frame, seed=0, tiles=(rank, ws), layout=abi.RT_LAYOUT_TILES,
+                     chunks=shard.chunks)
     else:
         st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
-    px_launch = shard.tiles_per_rank * 64 if tiles_mode else W * H
+    px_launch = shard.tiles_per_rank * shard.chunks * 64 if tiles_mode else W * H
     bytes_launch = algorithmic_bytes(st, info, px_launch)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
@@ -283,8 +287,9 @@ def main():
         "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
                    "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
                    "parallelism": ("1 GPU" if ws == 1 else
-                                   "tile-shard x%d (tile t on rank t %% %d) + %s gather" % (
-                                       ws, ws, "RCCL" if args.backend == "nccl" else "gloo")
+                                   "tile-shard x%d (tile t on rank t %% %d, %d stratum chunks) + %s gather" % (
+                                       ws, ws, shard.chunks,
+                                       "RCCL" if args.backend == "nccl" else "gloo")
                                    if tiles_mode else
                                    "stratum-shard x%d + %s reduce(sum)" % (
                                        ws, "RCCL" if args.backend == "nccl" else "gloo"))},

@@ -214,7 +214,11 @@ typedef struct rt_render_params {
                            RT_LAYOUT_TILES: the k-th rendered tile's 64 pixels at
                            [k*64, k*64+64), pixel (x,y) of the tile at k*64 + y*8 + x
                            (slots outside the image hold 0) */
-  int32_t _pad;
+  int32_t strata_chunks; /* RT_LAYOUT_TILES only: split each tile's strata into this
+                            many equal consecutive chunks, each traced by its own
+                            wavefront (finer work units for small tile subsets);
+                            the output becomes [tile k][chunk c][64 px][3], whose
+                            chunk sums are the tile's sums.  0 or 1 = one chunk. */
 } rt_render_params;
 
 /* Per-launch traversal/shading counters (for algorithmic-bytes accounting). */

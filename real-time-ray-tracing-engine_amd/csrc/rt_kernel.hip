@@ -66,9 +66,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
     for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
   }
-  const int local_tile = blockIdx.x * kWaves + wv;
-  if (local_tile >= P.n_local_tiles) return; // whole wave exits together
+  const int unit = blockIdx.x * kWaves + wv; // work unit = (local tile, stratum chunk)
+  if (unit >= P.n_local_tiles * P.n_chunks) return; // whole wave exits together
+  const int local_tile = unit / P.n_chunks, chunk = unit - local_tile * P.n_chunks;
   const int tile = P.tile_first + local_tile * P.tile_stride;
+  const int s_first = P.sample_begin + chunk * P.chunk_strata;
+  const int s_count = min(P.chunk_strata, P.sample_count - chunk * P.chunk_strata);
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
   const int x0 = tx * 8, y0 = P.row_begin + ty * 8;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
   Counters cnt{0, 0, 0, 0, 0, 0};
   uint32_t n_samples = 0, n_segments = 0;
 
-  const int n_items = 64 * P.sample_count;
+  const int n_items = 64 * max(0, s_count);
   int next_item = 0; // wave-uniform head of the tile's work queue
   PathState ps;
   ps.active = false;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
         int i = x0 + (slot & 7), j = y0 + (slot >> 3);
         if (i < C.W && j < P.row_end) {
           ps.slot = slot;
-          ps.sample = P.sample_begin + (item >> 6);
+          ps.sample = s_first + (item >> 6);
           key.pixel = (uint32_t)(j * C.W + i);
           key.sample = (uint32_t)ps.sample;
           ps.ray = camera_ray(C, key, i, j, ps.sample);
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
         sy = C.scale * sy;
         sz = C.scale * sz;
       }
-      double *o = P.compact ? out + 3 * ((size_t)local_tile * 64 + lane)
+      double *o = P.compact ? out + 3 * ((size_t)unit * 64 + lane)
                             : out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
       if (P.accumulate) {
         o[0] += sx;
@@ -156,6 +159,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
       if (lane == 0) atomicAdd(&stats[k], x);
     }
   }
+}
+
+// Frame assembly after a chunked launch (rtk_launch_render_chunked): each
+// pixel's stratum-chunk partial sums, added in chunk order, become the frame
+// pixel (scaled / accumulated as the launch asks).
+__global__ void chunk_sum_kernel(const double *parts, DCamera C, DLaunch P, int n_chunks,
+                                 double *out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int rows = P.row_end - P.row_begin;
+  if (idx >= (int64_t)C.W * rows * 3) return;
+  const int ch = (int)(idx % 3);
+  const int64_t pix = idx / 3;
+  const int i = (int)(pix % C.W), jr = (int)(pix / C.W);
+  const int tile = (jr >> 3) * P.tiles_x + (i >> 3), slot = ((jr & 7) << 3) | (i & 7);
+  const double *p = parts + ((size_t)tile * n_chunks * 64 + slot) * 3 + ch;
+  double sum = p[0];
+  for (int k = 1; k < n_chunks; ++k) sum += p[(size_t)k * 64 * 3];
+  if (P.output == RT_OUT_SCALED) sum = C.scale * sum;
+  out[idx] = P.accumulate ? out[idx] + sum : sum;
 }
 
 __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint8_t *bytes) {
@@ -197,7 +219,8 @@ extern "C" size_t rtk_lds_bytes(int stack_depth, int n_lds_nodes) {
 
 // LDS bytes per block left for the staged BVH prefix at the occupancy the
 // instance's register count allows (blocks of kWaves waves, one per SIMD).
-extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes) {
+extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
+                                      int *waves_per_simd_out) {
   hipFuncAttributes a;
   hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(render_table(false)[features & F_ALL]));
   if (e != hipSuccess) return e;
@@ -205,6 +228,7 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
   int waves_per_simd = regs > 0 ? 512 / regs : 8;
   if (waves_per_simd > 8) waves_per_simd = 8;
   if (waves_per_simd < 1) waves_per_simd = 1;
+  *waves_per_simd_out = waves_per_simd;
   const size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
   size_t per_block = lds_cu / waves_per_simd;
   if (per_block > cap) per_block = cap;
@@ -216,11 +240,32 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
-  int blocks = (P->n_local_tiles + kWaves - 1) / kWaves;
+  int blocks = (P->n_local_tiles * P->n_chunks + kWaves - 1) / kWaves;
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->stack_depth, S->n_lds_nodes);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, *P, out, stats);
+  return hipGetLastError();
+}
+
+// Frame-layout launch split into (tile, stratum chunk) work units: finer units
+// shorten the tail of the last wave round; partials go to `scratch`
+// ([tiles][n_chunks][64][3]) and chunk_sum_kernel assembles the frame.
+extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
+                                                const DLaunch *P, int n_chunks, double *out,
+                                                double *scratch, hipStream_t stream) {
+  DLaunch Q = *P;
+  Q.compact = 1;
+  Q.accumulate = 0;
+  Q.output = RT_OUT_SUM;
+  Q.n_chunks = n_chunks;
+  Q.chunk_strata = (P->sample_count + n_chunks - 1) / n_chunks;
+  hipError_t e = rtk_launch_render(S, C, &Q, scratch, nullptr, stream);
+  if (e != hipSuccess) return e;
+  int64_t total = (int64_t)C->W * (P->row_end - P->row_begin) * 3;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                     scratch, *C, *P, n_chunks, out);
   return hipGetLastError();
 }
 

@@ -155,6 +155,7 @@ struct DLaunch {
   int32_t tile_first, tile_stride; // tiles rendered: tile_first + k * tile_stride
   int32_t n_local_tiles;           // k in [0, n_local_tiles)
   int32_t compact;                 // RT_LAYOUT_TILES output
+  int32_t n_chunks, chunk_strata;  // work unit = (tile, stratum chunk); compact only
 };
 
 #endif

@@ -85,7 +85,7 @@ class RenderParams(C.Structure):
                 ("sample_begin", C.c_int32), ("sample_count", C.c_int32),
                 ("seed", C.c_uint64), ("output", C.c_int32), ("accumulate", C.c_int32),
                 ("tile_first", C.c_int32), ("tile_stride", C.c_int32),
-                ("layout", C.c_int32), ("_pad", C.c_int32)]
+                ("layout", C.c_int32), ("strata_chunks", C.c_int32)]
 
 
 RT_LAYOUT_FRAME, RT_LAYOUT_TILES = 0, 1

@@ -81,44 +81,63 @@ def tiles_to_frame(gathered, width, height):
     return img[:height, :width]
 
 
+def auto_chunks(frame, world, target_units=65536):
+    """Stratum chunks per tile so one rank still has ~target_units wavefront work
+    units (several per wave slot of the 256-CU chip): a rank of an 8-way split
+    holds few tiles, and one wave per slot would make the slowest tile the
+    kernel time."""
+    n, t_r = tile_counts(frame, world)
+    strata = frame.sqrt_spp * frame.sqrt_spp
+    c = max(1, min(strata, -(-target_units // max(1, t_r))))
+    cs = -(-strata // c)  # strata per chunk; no empty chunks
+    return -(-strata // cs)
+
+
 class TileShardedRenderer:
     """Renders one frame per call with tile t on rank t % world.
 
-    render_fn(frame, buf, seed, tiles=(first, stride)) must overwrite `buf`
-    ([T_r, 64, 3] float64) with the raw sums of all strata of those tiles in
-    RT_LAYOUT_TILES order (Renderer.render_device with output=RT_OUT_SUM,
-    accumulate=0, layout=RT_LAYOUT_TILES)."""
+    render_fn(frame, buf, seed, tiles=(first, stride), chunks) must overwrite
+    `buf` ([T_r, chunks, 64, 3] float64) with the raw sums of all strata of
+    those tiles in RT_LAYOUT_TILES order, each tile's strata split into
+    `chunks` (Renderer.render_device with output=RT_OUT_SUM, accumulate=0,
+    layout=RT_LAYOUT_TILES, chunks=chunks)."""
 
-    def __init__(self, render_fn, frame, rank=0, world=1):
+    def __init__(self, render_fn, frame, rank=0, world=1, chunks=None):
         self.render_fn = render_fn
         self.frame = frame
         self.rank, self.world = rank, world
         self.n_tiles, self.tiles_per_rank = tile_counts(frame, world)
+        self.chunks = auto_chunks(frame, world) if chunks is None else max(1, chunks)
 
     def buffer(self, device=None):
-        return torch.zeros((self.tiles_per_rank, 64, 3), dtype=torch.float64, device=device)
+        return torch.zeros((self.tiles_per_rank, self.chunks, 64, 3), dtype=torch.float64,
+                           device=device)
 
     def gather_buffer(self, device=None):
         return torch.zeros((self.world, self.tiles_per_rank, 64, 3), dtype=torch.float64,
                            device=device)
 
     def render(self, buf, seed):
-        self.render_fn(self.frame, buf, seed, (self.rank, self.world))
+        """Render this rank's tiles; returns the per-tile sums [T_r, 64, 3] (the
+        chunk sum, in fixed chunk order)."""
+        self.render_fn(self.frame, buf, seed, (self.rank, self.world), self.chunks)
+        return buf[:, 0] if self.chunks == 1 else buf.sum(dim=1)
 
-    def gather(self, buf, gathered=None, async_op=False):
-        """Collect every rank's tiles on rank 0 (gathered: [world, T_r, 64, 3])."""
+    def gather(self, tiles, gathered=None, async_op=False):
+        """Collect every rank's [T_r, 64, 3] tile sums on rank 0 (gathered:
+        [world, T_r, 64, 3])."""
         if self.world == 1:
-            gathered[0].copy_(buf)
+            gathered[0].copy_(tiles)
             return None
         parts = list(gathered.unbind(0)) if self.rank == 0 else None
-        return dist.gather(buf, gather_list=parts, dst=0, async_op=async_op)
+        return dist.gather(tiles.contiguous(), gather_list=parts, dst=0, async_op=async_op)
 
     def frame_sums(self, gathered):
         return tiles_to_frame(gathered, self.frame.image_width, self.frame.image_height)
 
     def step(self, buf, gathered, seed):
-        self.render(buf, seed)
-        self.gather(buf, gathered)
+        tiles = self.render(buf, seed)
+        self.gather(tiles, gathered)
         return self.frame_sums(gathered) if self.rank == 0 else None
 
 

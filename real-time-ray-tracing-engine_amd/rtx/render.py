@@ -58,7 +58,7 @@ class Renderer:
 
     @staticmethod
     def params(seed=0, rows=(0, 0), samples=(0, -1), output=abi.RT_OUT_SCALED, accumulate=0,
-               tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME):
+               tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME, chunks=1):
         p = abi.RenderParams()
         p.row_begin, p.row_end = int(rows[0]), int(rows[1])
         p.sample_begin, p.sample_count = int(samples[0]), int(samples[1])
@@ -67,6 +67,7 @@ class Renderer:
         p.accumulate = int(accumulate)
         p.tile_first, p.tile_stride = int(tiles[0]), int(tiles[1])
         p.layout = int(layout)
+        p.strata_chunks = int(chunks)
         return p
 
     @staticmethod
@@ -80,33 +81,37 @@ class Renderer:
         return max(0, (n - first + stride - 1) // stride)
 
     def render(self, frame, seed=0, rows=(0, 0), samples=(0, -1), output=abi.RT_OUT_SCALED,
-               tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME):
-        """Synchronous render -> float64 array [rows, W, 3] (frame layout) or
-        [tiles, 64, 3] (tile layout), on the host."""
+               tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME, chunks=1):
+        """Synchronous render -> float64 array [rows, W, 3] (frame layout),
+        [tiles, 64, 3] (tile layout) or [tiles, chunks, 64, 3] (chunks > 1), on
+        the host."""
         r0, r1 = rows
         if r0 == 0 and r1 == 0:  # the ABI's "whole image"
             r1 = frame.image_height
         if layout == abi.RT_LAYOUT_TILES:
-            out = np.zeros((self.local_tiles(frame, rows, tiles), 64, 3), dtype=np.float64)
+            n = self.local_tiles(frame, rows, tiles)
+            shape = (n, 64, 3) if chunks <= 1 else (n, chunks, 64, 3)
+            out = np.zeros(shape, dtype=np.float64)
         else:
             out = np.empty((max(0, r1 - r0), frame.image_width, 3), dtype=np.float64)
-        p = self.params(seed, (r0, r1), samples, output, 0, tiles, layout)
+        p = self.params(seed, (r0, r1), samples, output, 0, tiles, layout, chunks)
         check(self.lib.rt_render(self.handle, C.byref(frame), C.byref(p),
                                  out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 
     def render_device(self, frame, dev_ptr, stream_ptr=None, seed=0, rows=(0, 0), samples=(0, -1),
-                      output=abi.RT_OUT_SUM, accumulate=1, tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME):
+                      output=abi.RT_OUT_SUM, accumulate=1, tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME,
+                      chunks=1):
         """Asynchronous render into a device buffer (e.g. a torch.cuda tensor's
         data_ptr()) on `stream_ptr` (0/None = the HIP null stream)."""
-        p = self.params(seed, rows, samples, output, accumulate, tiles, layout)
+        p = self.params(seed, rows, samples, output, accumulate, tiles, layout, chunks)
         check(self.lib.rt_render_device(self.handle, C.byref(frame), C.byref(p),
                                         C.c_void_p(dev_ptr), C.c_void_p(stream_ptr or 0)))
 
     def stats(self, frame, seed=0, rows=(0, 0), samples=(0, -1), tiles=(0, 1),
-              layout=abi.RT_LAYOUT_FRAME):
+              layout=abi.RT_LAYOUT_FRAME, chunks=1):
         s = abi.PathStats()
-        p = self.params(seed, rows, samples, tiles=tiles, layout=layout)
+        p = self.params(seed, rows, samples, tiles=tiles, layout=layout, chunks=chunks)
         check(self.lib.rt_render_stats(self.handle, C.byref(frame), C.byref(p), C.byref(s)))
         return {k: getattr(s, k) for k, _ in abi.PathStats._fields_}
 

@@ -118,14 +118,18 @@ def _tile_worker(rank, world, port, out_path):
         cam = S.camera_desc(image_width=27, samples_per_pixel=4, max_depth=6)
         from rtx.render import camera_frame
         frame = camera_frame(cam)
-        full = O.oracle_render(S, cam, O.MODE_COUNTER, 3, output=abi.RT_OUT_SUM)
+        chunks = 2  # 4 strata -> 2 chunks of 2, as the kernel splits them
+        parts = [O.oracle_render(S, cam, O.MODE_COUNTER, 3, samples=(2 * c, 2),
+                                 output=abi.RT_OUT_SUM) for c in range(chunks)]
 
-        def render_fn(fr, buf, seed, tiles):
-            tl = frame_to_tiles(full, tiles[0], tiles[1])
+        def render_fn(fr, buf, seed, tiles, n_chunks):
+            assert n_chunks == chunks
             buf.zero_()
-            buf[:len(tl)] = torch.from_numpy(tl)
+            for c in range(chunks):
+                tl = frame_to_tiles(parts[c], tiles[0], tiles[1])
+                buf[:len(tl), c] = torch.from_numpy(tl)
 
-        tr = TileShardedRenderer(render_fn, frame, rank, world)
+        tr = TileShardedRenderer(render_fn, frame, rank, world, chunks=chunks)
         buf, g = tr.buffer(), tr.gather_buffer()
         img = tr.step(buf, g, seed=3)
         if rank == 0:
@@ -140,7 +144,9 @@ def test_two_rank_gloo_tile_sharding_reassembles_the_frame(tmp_path):
     S = load_scene(SCENE)
     cam = S.camera_desc(image_width=27, samples_per_pixel=4, max_depth=6)
     want = O.oracle_render(S, cam, O.MODE_COUNTER, 3, output=abi.RT_OUT_SUM)
-    assert np.array_equal(np.load(out), want, equal_nan=True)
+    got = np.load(out)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    np.testing.assert_allclose(np.nan_to_num(got), np.nan_to_num(want), rtol=1e-12, atol=1e-14)
 
 
 @pytest.mark.gpu
@@ -150,7 +156,13 @@ def test_gpu_tile_layout_reassembles_bit_exact():
     cam = S.camera_desc(image_width=44, samples_per_pixel=9, max_depth=6)  # ragged: 44 = 5.5 tiles
     f = camera_frame(cam)
     with Renderer(S) as R:
-        full = R.render(f, seed=6, output=abi.RT_OUT_SUM)
+        os.environ["RTX_CHUNK_TARGET"] = "0"  # one work unit per tile: same sums bit for bit
+        try:
+            full = R.render(f, seed=6, output=abi.RT_OUT_SUM)
+        finally:
+            del os.environ["RTX_CHUNK_TARGET"]
+        chunked = R.render(f, seed=6, output=abi.RT_OUT_SUM)  # library's auto chunking
+        np.testing.assert_allclose(chunked, full, rtol=1e-12, atol=1e-13)
         world = 3
         n, t_r = tile_counts(f, world)
         g = np.zeros((world, t_r, 64, 3))
@@ -161,3 +173,11 @@ def test_gpu_tile_layout_reassembles_bit_exact():
             g[r, :len(tl)] = tl
     assert np.array_equal(tiles_to_frame(torch.from_numpy(g), f.image_width, f.image_height).numpy(),
                           full)
+    # stratum chunks: per-chunk partial sums add up to the tile sums
+    with Renderer(S) as R:
+        ch = R.render(f, seed=6, output=abi.RT_OUT_SUM, tiles=(1, world), layout=abi.RT_LAYOUT_TILES,
+                      chunks=4)  # 9 strata -> chunks of 3, 3, 3, 0
+        assert ch.shape[1] == 4 and not ch[:, 3].any()
+        one = R.render(f, seed=6, output=abi.RT_OUT_SUM, tiles=(1, world),
+                       layout=abi.RT_LAYOUT_TILES)
+    np.testing.assert_allclose(ch.sum(axis=1), one, rtol=1e-12, atol=1e-13)
