@@ -149,7 +149,15 @@ typedef struct rt_scene_desc {
   int32_t use_bvh; /* reference -b: lights become HittableList(BVHNode(lights))
                       (StaticCamera.cpp:35-40); the world is always traversed through
                       the library's own BVH (closest hit is structure independent) */
+  int32_t bvh_builder; /* RT_BVH_AUTO (0): device LBVH from 65536 world primitives,
+                          host SAH below; RT_BVH_HOST; RT_BVH_DEVICE */
 } rt_scene_desc;
+
+enum {
+  RT_BVH_AUTO = 0,
+  RT_BVH_HOST = 1,  /* binned SAH on the host (rt_scene.cpp) */
+  RT_BVH_DEVICE = 2 /* linear BVH on the GPU (rt_bvh_build.hip) */
+};
 
 /* ---- camera (CameraConfig.hpp:9-35) ------------------------------------- */
 typedef struct rt_camera_desc {
@@ -244,6 +252,8 @@ typedef struct rt_scene_info {
   int64_t device_bytes; /* total device bytes of the scene */
   int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise */
   int32_t lds_nodes;    /* BVH nodes (BFS prefix) the kernel stages in LDS per block */
+  int32_t bvh_builder;  /* the builder that made the world BVH: RT_BVH_HOST / RT_BVH_DEVICE */
+  int32_t _pad;
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

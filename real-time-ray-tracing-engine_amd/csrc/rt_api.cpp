@@ -24,6 +24,11 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         hipStream_t stream);
 extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
                                       int *waves_per_simd);
+extern "C" size_t rtk_lbvh_temp_bytes(int n);
+extern "C" hipError_t rtk_build_lbvh(const double *boxes, const DItem *items_in, int n,
+                                     const double *scene_lo, const double *scene_hi,
+                                     DNode *nodes, DItem *items_out, int *depth_dev, void *temp,
+                                     size_t temp_bytes, hipStream_t st);
 extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
                                                 const DLaunch *P, int n_chunks, double *out,
                                                 double *scratch, hipStream_t stream);
@@ -180,6 +185,36 @@ int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame) {
   return RT_OK;
 }
 
+// Runs rtk_build_lbvh over the scene's world items (uploaded in scene order at
+// `items`): writes the nodes and the items in leaf order in place.
+static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *nodes,
+                                   DItem *items, int *depth) {
+  const int n = (int)H.items.size();
+  const size_t a_box = (6 * sizeof(double) * n + 255) & ~size_t(255);
+  const size_t a_items = (sizeof(DItem) * n + 255) & ~size_t(255);
+  const size_t lb = rtk_lbvh_temp_bytes(n);
+  const size_t total = a_box + a_items + 256 + lb;
+  char *tmp = nullptr;
+  hipError_t e = hipMalloc((void **)&tmp, total);
+  if (e != hipSuccess) return e;
+  double *d_box = (double *)tmp;
+  DItem *d_sorted = (DItem *)(tmp + a_box);
+  int *d_depth = (int *)(tmp + a_box + a_items);
+  void *d_lb = tmp + a_box + a_items + 256;
+  e = hipMemcpyAsync(d_box, H.item_boxes.data(), 6 * sizeof(double) * n, hipMemcpyHostToDevice,
+                     s->stream);
+  if (e == hipSuccess)
+    e = rtk_build_lbvh(d_box, items, n, H.scene_lo, H.scene_hi, nodes, d_sorted, d_depth, d_lb, lb,
+                       s->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(items, d_sorted, sizeof(DItem) * n, hipMemcpyDeviceToDevice, s->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(depth, d_depth, sizeof(int), hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipFree(tmp);
+  return e;
+}
+
 int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   if (!out) return set_err(RT_ERR_INVALID, "null output pointer");
   *out = nullptr;
@@ -277,6 +312,37 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
   if (const char *fx = std::getenv("RTX_EXTRA_FEATURES")) // debug: widen the instance
     d.features |= std::atoi(fx) & 15;
+  // device-built world BVH (rt_bvh_build.hip), host SAH fallback if the linear
+  // tree is deeper than the traversal stack
+  int builder = RT_BVH_HOST;
+  if (H.device_bvh) {
+    int depth = -1;
+    hipError_t be = device_bvh_build(s, H, (DNode *)P(iN), (DItem *)P(iI), &depth);
+    if (be != hipSuccess) {
+      rt_scene_destroy(s);
+      return hip_err(be, "device BVH build");
+    }
+    int max_depth = RT_STACK_DEPTH - 1;
+    if (const char *md = std::getenv("RTX_LBVH_MAX_DEPTH")) max_depth = std::atoi(md); // tests
+    if (depth >= 0 && depth <= max_depth) {
+      H.bvh_depth = depth;
+      builder = RT_BVH_DEVICE;
+    } else { // too deep for the per-lane stack: rebuild on the host (depth-capped SAH)
+      rtx::build_world_bvh_host(H);
+      hipError_t ue = hipMemcpy((void *)P(iN), H.nodes.data(), H.nodes.size() * sizeof(DNode),
+                                hipMemcpyHostToDevice);
+      if (ue == hipSuccess)
+        ue = hipMemcpy((void *)P(iI), H.items.data(), H.items.size() * sizeof(DItem),
+                       hipMemcpyHostToDevice);
+      if (ue != hipSuccess) {
+        rt_scene_destroy(s);
+        return hip_err(ue, "BVH upload");
+      }
+    }
+    d.n_nodes = (int32_t)H.nodes.size();
+    d.root_is_leaf = H.root_is_leaf;
+    d.n_root_items = H.n_root_items;
+  }
   // traversal stack: one entry per BVH level suffices (a pushed entry is the
   // sibling of a node on the current root path); LDS prefix of the BFS-ordered
   // nodes sized to what the instance's occupancy leaves free
@@ -310,6 +376,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.device_bytes = (int64_t)off;
   in.features = d.features;
   in.lds_nodes = d.n_lds_nodes;
+  in.bvh_builder = builder;
   *out = s;
   return RT_OK;
 }

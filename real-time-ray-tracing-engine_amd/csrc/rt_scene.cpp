@@ -93,6 +93,201 @@ int bx_longest(const Bx &b) {
   return sy > sz ? 1 : 2;
 }
 
+// ---------------------------------------------------------------- world BVH
+// Host binned-SAH builder (also the fallback of the device LBVH builder).
+struct SahBuilder {
+  HostScene &H;
+  explicit SahBuilder(HostScene &h) : H(h) {}
+
+  struct BRef {
+    Bx b;
+    P3 c;
+    int32_t obj;
+  };
+  struct BNode {
+    Bx b;
+    int left = -1, right = -1; // build-node indices, -1 for leaves
+    int first = 0, count = 0;  // leaf ref range
+  };
+  std::vector<BNode> bn;
+  int max_depth_seen = 0;
+
+  int build(std::vector<BRef> &r, int st, int en, int dep) {
+    BNode n;
+    n.b = bx_empty();
+    Bx cb = bx_empty();
+    for (int i = st; i < en; ++i) {
+      n.b = bx_join(n.b, r[i].b);
+      Bx pc{{r[i].c.x, r[i].c.y, r[i].c.z}, {r[i].c.x, r[i].c.y, r[i].c.z}};
+      cb = bx_join(cb, pc);
+    }
+    int cnt = en - st;
+    max_depth_seen = std::max(max_depth_seen, dep);
+    int id = (int)bn.size();
+    bn.push_back(n);
+    const int kLeafMax = 2;
+    if (cnt <= kLeafMax) {
+      bn[id].first = st;
+      bn[id].count = cnt;
+      return id;
+    }
+    // depth budget: switch to balanced median splits when the SAH tree risks
+    // exceeding the per-lane traversal stack (RT_STACK_DEPTH)
+    int need = 0;
+    while ((1 << need) < cnt) ++need;
+    bool force_median = dep + need >= RT_STACK_DEPTH - 2;
+    int best_axis = -1, best_bin = -1;
+    double best_cost = kInf;
+    const int kBins = 16;
+    if (!force_median) {
+      for (int ax = 0; ax < 3; ++ax) {
+        double lo = cb.lo[ax], hi = cb.hi[ax];
+        if (!(hi - lo > 1e-12)) continue;
+        Bx bb[kBins];
+        int bc[kBins];
+        for (int k = 0; k < kBins; ++k) {
+          bb[k] = bx_empty();
+          bc[k] = 0;
+        }
+        double sc = kBins / (hi - lo);
+        for (int i = st; i < en; ++i) {
+          int k = std::min(kBins - 1, std::max(0, (int)((comp(r[i].c, ax) - lo) * sc)));
+          bb[k] = bx_join(bb[k], r[i].b);
+          bc[k]++;
+        }
+        Bx lb[kBins];
+        int lc[kBins];
+        Bx acc = bx_empty();
+        int a = 0;
+        for (int k = 0; k < kBins; ++k) {
+          acc = bx_join(acc, bb[k]);
+          a += bc[k];
+          lb[k] = acc;
+          lc[k] = a;
+        }
+        acc = bx_empty();
+        a = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          acc = bx_join(acc, bb[k]);
+          a += bc[k];
+          int nl = lc[k - 1], nr = a;
+          if (nl == 0 || nr == 0) continue;
+          double cost = bx_area(lb[k - 1]) * nl + bx_area(acc) * nr;
+          if (cost < best_cost) {
+            best_cost = cost;
+            best_axis = ax;
+            best_bin = k;
+          }
+        }
+      }
+    }
+    int mid;
+    if (best_axis >= 0) {
+      double lo = cb.lo[best_axis], hi = cb.hi[best_axis];
+      double sc = kBins / (hi - lo);
+      auto it = std::partition(r.begin() + st, r.begin() + en, [&](const BRef &x) {
+        int k = std::min(kBins - 1, std::max(0, (int)((comp(x.c, best_axis) - lo) * sc)));
+        return k < best_bin;
+      });
+      mid = int(it - r.begin());
+      // leaf if splitting does not pay (SAH with traversal cost 1, isect cost 1)
+      double parent_area = bx_area(bn[id].b);
+      if (cnt <= 4 && parent_area > 0 && 1.0 + best_cost / parent_area >= (double)cnt) {
+        bn[id].first = st;
+        bn[id].count = cnt;
+        return id;
+      }
+    } else {
+      mid = st + cnt / 2;
+    }
+    if (mid <= st || mid >= en) {
+      int ax = bx_longest(cb);
+      std::sort(r.begin() + st, r.begin() + en,
+                [ax](const BRef &a, const BRef &b) { return comp(a.c, ax) < comp(b.c, ax); });
+      mid = st + cnt / 2;
+    }
+    int L = build(r, st, mid, dep + 1);
+    int R = build(r, mid, en, dep + 1);
+    bn[id].left = L;
+    bn[id].right = R;
+    return id;
+  }
+
+  // fp32 box bounds rounded outward, widened by a relative 2^-20 plus 1e-7 so
+  // the conservative fp32 slab test (rt_path.h) can never reject a box whose
+  // primitives the fp64 test would hit.
+  static float f32_lo(double x) {
+    double m = x - (std::fabs(x) * 0x1p-20 + 1e-7);
+    float f = (float)m;
+    if ((double)f > m) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+  }
+  static float f32_hi(double x) {
+    double m = x + (std::fabs(x) * 0x1p-20 + 1e-7);
+    float f = (float)m;
+    if ((double)f < m) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+  }
+
+  void emit_world_bvh(const std::vector<Bx> &item_box) {
+    std::vector<BRef> r;
+    for (size_t i = 0; i < item_box.size(); ++i) {
+      BRef x;
+      x.b = item_box[i];
+      x.c = bx_center(x.b);
+      x.obj = (int32_t)i;
+      r.push_back(x);
+    }
+    if (r.empty()) {
+      H.root_is_leaf = 1;
+      H.n_root_items = 0;
+      return;
+    }
+    bn.clear();
+    int root = build(r, 0, (int)r.size(), 0);
+    H.bvh_depth = max_depth_seen;
+    // store the items in leaf order: a leaf is a contiguous item range
+    std::vector<DItem> leaf_order;
+    leaf_order.reserve(r.size());
+    for (auto &x : r) leaf_order.push_back(H.items[x.obj]);
+    H.items.swap(leaf_order);
+    if (bn[root].left < 0) {
+      H.root_is_leaf = 1;
+      H.n_root_items = bn[root].count;
+      return;
+    }
+    // flatten in BFS order (the top levels come first: they are the nodes every
+    // ray visits, and the kernel stages a prefix of the array in LDS); each DNode
+    // holds both children's boxes
+    std::vector<int> map(bn.size(), -1);
+    std::vector<int> order;
+    order.push_back(root);
+    for (size_t q = 0; q < order.size(); ++q) {
+      const BNode &p = bn[order[q]];
+      map[order[q]] = (int)q;
+      if (bn[p.left].left >= 0) order.push_back(p.left);
+      if (bn[p.right].left >= 0) order.push_back(p.right);
+    }
+    H.nodes.resize(order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+      const BNode &p = bn[order[i]];
+      DNode &d = H.nodes[i];
+      std::memset(&d, 0, sizeof d);
+      int ch[2] = {p.left, p.right};
+      for (int k = 0; k < 2; ++k) {
+        const BNode &c = bn[ch[k]];
+        float *lo = k ? d.lo1 : d.lo0, *hi = k ? d.hi1 : d.hi0;
+        for (int a = 0; a < 3; ++a) {
+          lo[a] = f32_lo(c.b.lo[a]);
+          hi[a] = f32_hi(c.b.hi[a]);
+        }
+        d.entry[k] = c.left < 0 ? ~((c.first << 3) | c.count) : map[ch[k]];
+      }
+    }
+  }
+
+};
+
 struct Compiler {
   const rt_scene_desc *D;
   HostScene &H;
@@ -494,194 +689,6 @@ struct Compiler {
     }
   }
 
-  // ---------------------------------------------------------------- world BVH
-  struct BRef {
-    Bx b;
-    P3 c;
-    int32_t obj;
-  };
-  struct BNode {
-    Bx b;
-    int left = -1, right = -1; // build-node indices, -1 for leaves
-    int first = 0, count = 0;  // leaf ref range
-  };
-  std::vector<BNode> bn;
-  int max_depth_seen = 0;
-
-  int build(std::vector<BRef> &r, int st, int en, int dep) {
-    BNode n;
-    n.b = bx_empty();
-    Bx cb = bx_empty();
-    for (int i = st; i < en; ++i) {
-      n.b = bx_join(n.b, r[i].b);
-      Bx pc{{r[i].c.x, r[i].c.y, r[i].c.z}, {r[i].c.x, r[i].c.y, r[i].c.z}};
-      cb = bx_join(cb, pc);
-    }
-    int cnt = en - st;
-    max_depth_seen = std::max(max_depth_seen, dep);
-    int id = (int)bn.size();
-    bn.push_back(n);
-    const int kLeafMax = 2;
-    if (cnt <= kLeafMax) {
-      bn[id].first = st;
-      bn[id].count = cnt;
-      return id;
-    }
-    // depth budget: switch to balanced median splits when the SAH tree risks
-    // exceeding the per-lane traversal stack (RT_STACK_DEPTH)
-    int need = 0;
-    while ((1 << need) < cnt) ++need;
-    bool force_median = dep + need >= RT_STACK_DEPTH - 2;
-    int best_axis = -1, best_bin = -1;
-    double best_cost = kInf;
-    const int kBins = 16;
-    if (!force_median) {
-      for (int ax = 0; ax < 3; ++ax) {
-        double lo = cb.lo[ax], hi = cb.hi[ax];
-        if (!(hi - lo > 1e-12)) continue;
-        Bx bb[kBins];
-        int bc[kBins];
-        for (int k = 0; k < kBins; ++k) {
-          bb[k] = bx_empty();
-          bc[k] = 0;
-        }
-        double sc = kBins / (hi - lo);
-        for (int i = st; i < en; ++i) {
-          int k = std::min(kBins - 1, std::max(0, (int)((comp(r[i].c, ax) - lo) * sc)));
-          bb[k] = bx_join(bb[k], r[i].b);
-          bc[k]++;
-        }
-        Bx lb[kBins];
-        int lc[kBins];
-        Bx acc = bx_empty();
-        int a = 0;
-        for (int k = 0; k < kBins; ++k) {
-          acc = bx_join(acc, bb[k]);
-          a += bc[k];
-          lb[k] = acc;
-          lc[k] = a;
-        }
-        acc = bx_empty();
-        a = 0;
-        for (int k = kBins - 1; k > 0; --k) {
-          acc = bx_join(acc, bb[k]);
-          a += bc[k];
-          int nl = lc[k - 1], nr = a;
-          if (nl == 0 || nr == 0) continue;
-          double cost = bx_area(lb[k - 1]) * nl + bx_area(acc) * nr;
-          if (cost < best_cost) {
-            best_cost = cost;
-            best_axis = ax;
-            best_bin = k;
-          }
-        }
-      }
-    }
-    int mid;
-    if (best_axis >= 0) {
-      double lo = cb.lo[best_axis], hi = cb.hi[best_axis];
-      double sc = kBins / (hi - lo);
-      auto it = std::partition(r.begin() + st, r.begin() + en, [&](const BRef &x) {
-        int k = std::min(kBins - 1, std::max(0, (int)((comp(x.c, best_axis) - lo) * sc)));
-        return k < best_bin;
-      });
-      mid = int(it - r.begin());
-      // leaf if splitting does not pay (SAH with traversal cost 1, isect cost 1)
-      double parent_area = bx_area(bn[id].b);
-      if (cnt <= 4 && parent_area > 0 && 1.0 + best_cost / parent_area >= (double)cnt) {
-        bn[id].first = st;
-        bn[id].count = cnt;
-        return id;
-      }
-    } else {
-      mid = st + cnt / 2;
-    }
-    if (mid <= st || mid >= en) {
-      int ax = bx_longest(cb);
-      std::sort(r.begin() + st, r.begin() + en,
-                [ax](const BRef &a, const BRef &b) { return comp(a.c, ax) < comp(b.c, ax); });
-      mid = st + cnt / 2;
-    }
-    int L = build(r, st, mid, dep + 1);
-    int R = build(r, mid, en, dep + 1);
-    bn[id].left = L;
-    bn[id].right = R;
-    return id;
-  }
-
-  // fp32 box bounds rounded outward, widened by a relative 2^-20 plus 1e-7 so
-  // the conservative fp32 slab test (rt_path.h) can never reject a box whose
-  // primitives the fp64 test would hit.
-  static float f32_lo(double x) {
-    double m = x - (std::fabs(x) * 0x1p-20 + 1e-7);
-    float f = (float)m;
-    if ((double)f > m) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-    return f;
-  }
-  static float f32_hi(double x) {
-    double m = x + (std::fabs(x) * 0x1p-20 + 1e-7);
-    float f = (float)m;
-    if ((double)f < m) f = std::nextafter(f, std::numeric_limits<float>::infinity());
-    return f;
-  }
-
-  void emit_world_bvh(const std::vector<Bx> &item_box) {
-    std::vector<BRef> r;
-    for (size_t i = 0; i < item_box.size(); ++i) {
-      BRef x;
-      x.b = item_box[i];
-      x.c = bx_center(x.b);
-      x.obj = (int32_t)i;
-      r.push_back(x);
-    }
-    if (r.empty()) {
-      H.root_is_leaf = 1;
-      H.n_root_items = 0;
-      return;
-    }
-    bn.clear();
-    int root = build(r, 0, (int)r.size(), 0);
-    H.bvh_depth = max_depth_seen;
-    // store the items in leaf order: a leaf is a contiguous item range
-    std::vector<DItem> leaf_order;
-    leaf_order.reserve(r.size());
-    for (auto &x : r) leaf_order.push_back(H.items[x.obj]);
-    H.items.swap(leaf_order);
-    if (bn[root].left < 0) {
-      H.root_is_leaf = 1;
-      H.n_root_items = bn[root].count;
-      return;
-    }
-    // flatten in BFS order (the top levels come first: they are the nodes every
-    // ray visits, and the kernel stages a prefix of the array in LDS); each DNode
-    // holds both children's boxes
-    std::vector<int> map(bn.size(), -1);
-    std::vector<int> order;
-    order.push_back(root);
-    for (size_t q = 0; q < order.size(); ++q) {
-      const BNode &p = bn[order[q]];
-      map[order[q]] = (int)q;
-      if (bn[p.left].left >= 0) order.push_back(p.left);
-      if (bn[p.right].left >= 0) order.push_back(p.right);
-    }
-    H.nodes.resize(order.size());
-    for (size_t i = 0; i < order.size(); ++i) {
-      const BNode &p = bn[order[i]];
-      DNode &d = H.nodes[i];
-      std::memset(&d, 0, sizeof d);
-      int ch[2] = {p.left, p.right};
-      for (int k = 0; k < 2; ++k) {
-        const BNode &c = bn[ch[k]];
-        float *lo = k ? d.lo1 : d.lo0, *hi = k ? d.hi1 : d.hi0;
-        for (int a = 0; a < 3; ++a) {
-          lo[a] = f32_lo(c.b.lo[a]);
-          hi[a] = f32_hi(c.b.hi[a]);
-        }
-        d.entry[k] = c.left < 0 ? ~((c.first << 3) | c.count) : map[ch[k]];
-      }
-    }
-  }
-
   // ------------------------------------------------------------ light leaves
   // BVHNode's split of a light list (BVHNode.cpp:21-123); returns a nested
   // description as a vector of (object, weight) pairs in DFS order.
@@ -851,20 +858,55 @@ struct Compiler {
       if (!make_item(f, it, bb)) return false;
       if (it.kind == I_MEDIUM) {
         H.mitems.push_back(it);
-        for (int a = 0; a < 3; ++a) H.mbox.push_back(f32_lo(bb.lo[a]));
-        for (int a = 0; a < 3; ++a) H.mbox.push_back(f32_hi(bb.hi[a]));
+        for (int a = 0; a < 3; ++a) H.mbox.push_back(SahBuilder::f32_lo(bb.lo[a]));
+        for (int a = 0; a < 3; ++a) H.mbox.push_back(SahBuilder::f32_hi(bb.hi[a]));
         continue;
       }
       H.items.push_back(it);
       ibox.push_back(bb);
     }
     emit_materials();
-    emit_world_bvh(ibox);
+    const int builder = D->bvh_builder;
+    const bool device = ibox.size() >= 2 &&
+                        (builder == RT_BVH_DEVICE ||
+                         (builder == RT_BVH_AUTO && ibox.size() >= (size_t)kDeviceBuildMin));
+    if (device) { // built by the library on the GPU after upload (rt_bvh_build.hip)
+      H.device_bvh = 1;
+      H.item_boxes.reserve(6 * ibox.size());
+      for (int a = 0; a < 3; ++a) {
+        H.scene_lo[a] = kInf;
+        H.scene_hi[a] = -kInf;
+      }
+      for (const Bx &bb : ibox) {
+        for (int a = 0; a < 3; ++a) H.item_boxes.push_back(bb.lo[a]);
+        for (int a = 0; a < 3; ++a) H.item_boxes.push_back(bb.hi[a]);
+        for (int a = 0; a < 3; ++a) { // centroid bounds (Morton grid)
+          double c = 0.5 * (bb.lo[a] + bb.hi[a]);
+          H.scene_lo[a] = std::fmin(H.scene_lo[a], c);
+          H.scene_hi[a] = std::fmax(H.scene_hi[a], c);
+        }
+      }
+      H.nodes.assign(ibox.size() - 1, DNode{});
+    } else {
+      SahBuilder(H).emit_world_bvh(ibox);
+    }
     return emit_lights();
   }
 };
 
 } // namespace
+
+void build_world_bvh_host(HostScene &H) {
+  std::vector<Bx> boxes(H.item_boxes.size() / 6);
+  for (size_t i = 0; i < boxes.size(); ++i)
+    for (int a = 0; a < 3; ++a) {
+      boxes[i].lo[a] = H.item_boxes[6 * i + a];
+      boxes[i].hi[a] = H.item_boxes[6 * i + 3 + a];
+    }
+  H.nodes.clear();
+  H.device_bvh = 0;
+  SahBuilder(H).emit_world_bvh(boxes);
+}
 
 int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err) {
   Compiler c(desc, out, err);

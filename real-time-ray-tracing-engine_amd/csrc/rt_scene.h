@@ -26,7 +26,19 @@ struct HostScene {
   int32_t root_is_leaf = 0;
   int32_t n_root_items = 0;
   int32_t bvh_depth = 0;
+  // device-built world BVH (rt_bvh_build.hip): items still in scene order, their
+  // boxes (lo xyz, hi xyz) and the centroid bounds; nodes sized, not filled
+  int32_t device_bvh = 0;
+  std::vector<double> item_boxes;
+  double scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
 };
+
+// Scenes with at least this many world primitives build their BVH on the
+// device when rt_scene_desc.bvh_builder is RT_BVH_AUTO.
+constexpr int kDeviceBuildMin = 65536;
+
+// Host SAH build from HostScene::item_boxes (fallback of the device build).
+void build_world_bvh_host(HostScene &H);
 
 // Returns RT_OK or an error code with `err` filled.
 int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err);

@@ -59,7 +59,11 @@ class SceneDesc(C.Structure):
                 ("materials", C.POINTER(MaterialDesc)), ("n_materials", C.c_int32),
                 ("n_objects", C.c_int32), ("objects", C.POINTER(ObjectDesc)),
                 ("children", C.POINTER(C.c_int32)), ("n_children", C.c_int32),
-                ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32)]
+                ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32),
+                ("bvh_builder", C.c_int32)]
+
+
+RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE = 0, 1, 2
 
 
 class CameraDesc(C.Structure):
@@ -103,7 +107,8 @@ class SceneInfo(C.Structure):
                 ("n_objects", C.c_int32), ("n_light_leaves", C.c_int32),
                 ("bvh_depth", C.c_int32), ("node_bytes", C.c_int32),
                 ("sphere_bytes", C.c_int32), ("quad_bytes", C.c_int32),
-                ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32)]
+                ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32),
+                ("bvh_builder", C.c_int32), ("_pad", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

@@ -93,6 +93,7 @@ class SceneDescription:
         self.world = -1
         self.lights = -1
         self.use_bvh = 0
+        self.bvh_builder = abi.RT_BVH_AUTO
         self.camera = None
         self._named_tex = {}
         self._named_mat = {}
@@ -144,6 +145,7 @@ class SceneDescription:
         d.objects, d.n_objects = O, len(self.objects)
         d.children, d.n_children = K, len(self.children)
         d.world, d.lights, d.use_bvh = self.world, self.lights, int(self.use_bvh)
+        d.bvh_builder = int(self.bvh_builder)
         return d
 
     def camera_desc(self, **overrides):

@@ -56,6 +56,7 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   rtx::HostScene H;
   std::string err;
   if (rtx::compile_scene(desc, H, err) != RT_OK) return -1;
+  if (H.device_bvh) rtx::build_world_bvh_host(H); // the device builder needs a GPU
   DScene S;
   S.nodes = H.nodes.data();
   S.items = H.items.data();
