@@ -36,15 +36,14 @@ static inline void oracle_philox4x32_10(const uint32_t ctr_in[4], const uint32_t
 }
 
 /* Two 53-bit uniforms in [0,1) from one Philox block. */
-static inline void oracle_philox_u01x2(uint64_t seed, uint32_t pixel, uint32_t sample,
-                                       uint32_t bounce, uint32_t slot, double out[2]) {
+// Four uniforms in [0,1) (x * 2^-32) from one Philox4x32-10 block for
+// (pixel, stratum, bounce, slot) — DESIGN.md "RNG contract".
+static inline void oracle_philox_u01x4(uint64_t seed, uint32_t pixel, uint32_t sample,
+                                       uint32_t bounce, uint32_t slot, double out[4]) {
   uint32_t ctr[4] = {pixel, sample, bounce, slot};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t x[4];
   oracle_philox4x32_10(ctr, key, x);
-  uint64_t a = ((uint64_t)x[0] << 32) | x[1];
-  uint64_t b = ((uint64_t)x[2] << 32) | x[3];
-  out[0] = (double)(a >> 11) * 0x1.0p-53;
-  out[1] = (double)(b >> 11) * 0x1.0p-53;
+  for (int k = 0; k < 4; ++k) out[k] = (double)x[k] * 0x1.0p-32;
 }
 #endif

@@ -160,7 +160,7 @@ enum { MODE_MT = 0, MODE_COUNTER = 1 };
 
 // Slots of the counter contract (DESIGN.md "RNG contract").
 static const uint32_t CAM_TAG = 0xFFFFFFFFu;
-enum { SLOT_EVENT = 0, SLOT_DIR = 1, SLOT_MEDIUM_BASE = 0x100 };
+enum { SLOT_SHADE = 0, SLOT_MEDIUM_BASE = 0x100 };
 
 struct Sampler {
   int mode;
@@ -173,8 +173,8 @@ struct Sampler {
   double rd(double a, double b) { return std::uniform_real_distribution<double>(a, b)(*eng); }
   int ri(int a, int b) { return std::uniform_int_distribution<int>(a, b)(*eng); }
   // ---- counter mode primitive
-  void ctr(uint32_t bnc, uint32_t slot, double out[2]) const {
-    oracle_philox_u01x2(seed, pixel, sample, bnc, slot, out);
+  void ctr(uint32_t bnc, uint32_t slot, double out[4]) const {
+    oracle_philox_u01x4(seed, pixel, sample, bnc, slot, out);
   }
 };
 
@@ -477,7 +477,7 @@ static bool medium_hit(const Ctx &C, const Obj *o, const Ray &r, Ival t, Hit &re
   if (s.mode == MODE_MT) {
     u = s.rd();
   } else {
-    double d[2];
+    double d[4];
     s.ctr(s.bounce, SLOT_MEDIUM_BASE + (uint32_t)o->id, d);
     u = d[0];
   }
@@ -687,16 +687,17 @@ static Cam cam_setup(const rt_camera_desc &cd) { // Camera.cpp:31-73
 static Ray get_ray(const Cam &c, Sampler &s, int i, int j, int si, int sj) { // Camera.cpp:186-216
   int sq = int(std::sqrt(c.spp));
   double rs = 1.0 / sq;
-  double a, b, tm;
+  double a, b, tm = 0;
   V disk{0, 0, 0};
   if (s.mode == MODE_MT) {
     a = s.rd();
     b = s.rd();
-  } else {
-    double d[2];
+  } else { // jitter and time from one block (slot 0)
+    double d[4];
     s.ctr(CAM_TAG, 0, d);
     a = d[0];
     b = d[1];
+    tm = d[2];
   }
   double px = ((si + a) * rs) - 0.5;
   double py = ((sj + b) * rs) - 0.5;
@@ -708,20 +709,14 @@ static Ray get_ray(const Cam &c, Sampler &s, int i, int j, int si, int sj) { // 
     if (s.mode == MODE_MT) {
       disk = mt_in_unit_disk(s);
     } else {
-      double d[2];
+      double d[4];
       s.ctr(CAM_TAG, 1, d);
       disk = ctr_in_unit_disk(d[0], d[1]);
     }
     org = c.center + (disk[0] * c.disk_u) + (disk[1] * c.disk_v); // Camera.cpp:226-230
   }
   V dir = ps - org;
-  if (s.mode == MODE_MT) {
-    tm = s.rd();
-  } else {
-    double d[2];
-    s.ctr(CAM_TAG, 2, d);
-    tm = d[0];
-  }
+  if (s.mode == MODE_MT) tm = s.rd();
   return Ray{org, dir, tm};
 }
 
@@ -743,9 +738,13 @@ static V ray_color(const Ctx &C, const Cam &cam, const Ray &r, int depth) { // C
     emitted = rec.front ? tex_value(S, M.texture, rec.u, rec.v, rec.p) : mk(0, 0, 0);
 
   double ev[2] = {0, 0}, dv[2] = {0, 0};
-  if (s.mode == MODE_COUNTER) {
-    s.ctr(s.bounce, SLOT_EVENT, ev);
-    s.ctr(s.bounce, SLOT_DIR, dv);
+  if (s.mode == MODE_COUNTER) { // one block per shading event: (e0, e1, d0, d1)
+    double d[4];
+    s.ctr(s.bounce, SLOT_SHADE, d);
+    ev[0] = d[0];
+    ev[1] = d[1];
+    dv[0] = d[2];
+    dv[1] = d[3];
   }
   V att;
   if (M.kind == RT_MAT_DIFFUSE_LIGHT) return emitted; // Material::scatter default false
@@ -1283,9 +1282,9 @@ int oracle_render(const rt_scene_desc *D, const rt_camera_desc *cd, int mode, ui
 void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   oracle_philox4x32_10(ctr, key, out);
 }
-void oracle_u01x2(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t slot,
-                  double out[2]) {
-  oracle_philox_u01x2(seed, pixel, sample, bounce, slot, out);
+void oracle_u01x4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t slot,
+                  double out[4]) {
+  oracle_philox_u01x4(seed, pixel, sample, bounce, slot, out);
 }
 unsigned char oracle_to_byte(double x) { // ColorUtility.hpp:11-26
   double g = (x > 0) ? std::sqrt(x) : 0;

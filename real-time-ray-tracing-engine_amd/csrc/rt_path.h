@@ -30,10 +30,13 @@
 
 namespace rtp {
 
+#ifndef RT_PHILOX_ROUNDS
+#define RT_PHILOX_ROUNDS 10 // Philox4x32-10 (Random123 default); other values: timing experiments only
+#endif
 constexpr double kInf = __builtin_huge_val();
 constexpr double kPi = 3.1415926535897932385;
 constexpr uint32_t kCamTag = 0xFFFFFFFFu;
-constexpr uint32_t kSlotEvent = 0, kSlotDir = 1, kSlotMediumBase = 0x100;
+constexpr uint32_t kSlotShade = 0, kSlotMediumBase = 0x100;
 
 struct V3 {
   double x, y, z;
@@ -82,7 +85,7 @@ struct Key {
 RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                          uint32_t k0, uint32_t k1, uint32_t out[4]) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -100,15 +103,13 @@ RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
   out[2] = c2;
   out[3] = c3;
 }
-// Two 53-bit uniforms in [0,1) for (bounce, slot) — DESIGN.md "RNG contract".
-RT_HD RT_FI void u01x2(const Key &k, uint32_t bounce, uint32_t slot, double &a,
-                                      double &b) {
+// Four uniforms in [0,1) (x * 2^-32, exact in fp64) from one Philox block for
+// (bounce, slot) — DESIGN.md "RNG contract".
+RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]) {
   uint32_t x[4];
   philox10(k.pixel, k.sample, bounce, slot, k.k0, k.k1, x);
-  uint64_t ua = ((uint64_t)x[0] << 32) | x[1];
-  uint64_t ub = ((uint64_t)x[2] << 32) | x[3];
-  a = (double)(ua >> 11) * 0x1.0p-53;
-  b = (double)(ub >> 11) * 0x1.0p-53;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) u[q] = (double)x[q] * 0x1.0p-32;
 }
 
 // ---------------------------------------------------------------- features
@@ -382,9 +383,9 @@ RT_HD bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tm
   if (t1 < 0) t1 = 0;
   double rl = sqrt(len2(r.d));
   double inside = (t2 - t1) * rl;
-  double u, unused;
-  u01x2(key, bounce, kSlotMediumBase + (uint32_t)M.id, u, unused);
-  double hd = M.neg_inv_density * log(u);
+  double uu[4];
+  u01x4(key, bounce, kSlotMediumBase + (uint32_t)M.id, uu);
+  double hd = M.neg_inv_density * log(uu[0]);
   if (hd > inside) return false;
   h.t = t1 + hd / rl;
   h.p = at(r, h.t);
@@ -730,9 +731,9 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     ps.T = ps.T * e;
     return false;
   }
-  double e0, e1, d0, d1;
-  u01x2(key, b, kSlotEvent, e0, e1);
-  u01x2(key, b, kSlotDir, d0, d1);
+  double rn[4]; // one block per shading event: (e0, e1, d0, d1)
+  u01x4(key, b, kSlotShade, rn);
+  const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   if (M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
     V3 refl = r.d - (2 * dot(r.d, h.n)) * h.n;
@@ -835,24 +836,24 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
 RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
   double rs = 1.0 / C.sqrt_spp;
-  double ja, jb;
-  u01x2(key, kCamTag, 0, ja, jb);
+  double jt[4]; // slot 0: jitter x, jitter y, time
+  u01x4(key, kCamTag, 0, jt);
+  const double ja = jt[0], jb = jt[1];
   double px = ((si + ja) * rs) - 0.5;
   double py = ((sj + jb) * rs) - 0.5;
   V3 ps = (ld3(C.p00) + ((i + px) * ld3(C.du))) + ((j + py) * ld3(C.dv)); // Camera.cpp:186-205
   V3 org = ld3(C.center);
   if (!(C.defocus_angle <= 0)) {
-    double a, b;
-    u01x2(key, kCamTag, 1, a, b);
+    double dk[4]; // slot 1: defocus disk (r^2, angle)
+    u01x4(key, kCamTag, 1, dk);
+    const double a = dk[0], b = dk[1];
     double rr = sqrt(a);
     double s, c;
     sincos(2.0 * kPi * b, &s, &c);
     double dx = rr * c, dy = rr * s;
     org = (org + (dx * ld3(C.disk_u))) + (dy * ld3(C.disk_v)); // Camera.cpp:226-230
   }
-  double tm, unused;
-  u01x2(key, kCamTag, 2, tm, unused);
-  return Ray{org, ps - org, tm};
+  return Ray{org, ps - org, jt[2]};
 }
 
 

@@ -37,7 +37,7 @@ def oracle():
         L.oracle_render.restype = C.c_int
         L.oracle_camera_setup.argtypes = [P(abi.CameraDesc), P(abi.Frame)]
         L.oracle_philox.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
-        L.oracle_u01x2.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+        L.oracle_u01x4.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                    P(C.c_double)]
         L.oracle_to_byte.argtypes = [C.c_double]
         L.oracle_to_byte.restype = C.c_ubyte
