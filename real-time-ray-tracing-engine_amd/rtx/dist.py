@@ -22,6 +22,8 @@ gloo for the CPU tests.  The counter-based RNG is keyed by the global stratum
 index, so the union of the shards is exactly the one-GPU sample set: the result
 equals a single-GPU render up to fp64 summation order.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -81,11 +83,13 @@ def tiles_to_frame(gathered, width, height):
     return img[:height, :width]
 
 
-def auto_chunks(frame, world, target_units=65536):
+def auto_chunks(frame, world, target_units=None):
     """Stratum chunks per tile so one rank still has ~target_units wavefront work
     units (several per wave slot of the 256-CU chip): a rank of an 8-way split
     holds few tiles, and one wave per slot would make the slowest tile the
     kernel time."""
+    if target_units is None:
+        target_units = int(os.environ.get("RTX_SHARD_UNITS", "32768"))
     n, t_r = tile_counts(frame, world)
     strata = frame.sqrt_spp * frame.sqrt_spp
     c = max(1, min(strata, -(-target_units // max(1, t_r))))
