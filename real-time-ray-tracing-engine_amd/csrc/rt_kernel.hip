@@ -33,7 +33,10 @@
 namespace {
 
 using namespace rtp;
-constexpr int kWaves = 4; // waves (tiles) per 256-thread block
+#ifndef RT_BLOCK_WAVES
+#define RT_BLOCK_WAVES 4
+#endif
+constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 
 // Occupancy target per instance (waves per SIMD): the compiler may spill a few
 // registers to reach it.  Measured: 4 for the plain instance (C3
@@ -47,7 +50,7 @@ constexpr int kWaves = 4; // waves (tiles) per 256-thread block
 #define RT_WAVES_PER_EU(F) ((F) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER)
 
 template <bool STATS, unsigned F>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   // dynamic LDS: traversal stacks [kWaves][S.stack_depth][64] ints, then the
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
@@ -218,7 +221,7 @@ extern "C" size_t rtk_lds_bytes(int stack_depth, int n_lds_nodes) {
 }
 
 // LDS bytes per block left for the staged BVH prefix at the occupancy the
-// instance's register count allows (blocks of kWaves waves, one per SIMD).
+// instance's register count allows (blocks of kWaves waves over the 4 SIMDs).
 extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
                                       int *waves_per_simd_out) {
   hipFuncAttributes a;
@@ -230,7 +233,8 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
   if (waves_per_simd < 1) waves_per_simd = 1;
   *waves_per_simd_out = waves_per_simd;
   const size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
-  size_t per_block = lds_cu / waves_per_simd;
+  const int blocks_per_cu = waves_per_simd * 4 / kWaves > 0 ? waves_per_simd * 4 / kWaves : 1;
+  size_t per_block = lds_cu / blocks_per_cu;
   if (per_block > cap) per_block = cap;
   size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(stack_depth, 0);
   *n_nodes = per_block > fixed ? (int)((per_block - fixed) / sizeof(DNode)) : 0;
