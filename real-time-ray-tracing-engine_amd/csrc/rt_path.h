@@ -774,7 +774,10 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   }
   // Lambertian (CosinePDF) or Isotropic (SpherePDF), mixed 50/50 with the lights
   const bool lamb = (M.kind == RT_MAT_LAMBERTIAN);
-  V3 att = tex_value<F>(S, M.tex, h.p);
+  // albedo: fetched early when a noise texture may run (its long evaluation
+  // overlaps less live state there), late otherwise (shorter live range)
+  V3 att;
+  if constexpr ((F & F_NOISE) != 0) att = tex_value<F>(S, M.tex, h.p);
   V3 w = unitv(h.n); // ONB(n), ONB.hpp:25-37
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
   V3 ov = unitv(cross(w, a));
@@ -827,6 +830,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     ps.T = ps.T * v3(0.0, 0.0, 0.0);             // (keeps an earlier NaN/inf alive)
     return false;
   }
+  if constexpr ((F & F_NOISE) == 0) att = tex_value<F>(S, M.tex, h.p);
   V3 wgt = (1 / pdf) * (spdf * att);
   ps.T = ps.T * wgt;
   ps.ray = Ray{h.p, gd, r.tm};
