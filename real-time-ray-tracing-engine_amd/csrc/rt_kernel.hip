@@ -33,6 +33,11 @@
 namespace {
 
 using namespace rtp;
+// Idle lanes that trigger a refill while other lanes still trace (measured:
+// 16 for the plain instance, C3 +4 %; the rich instances lose with any delay).
+#ifndef RT_REGEN_MIN
+#define RT_REGEN_MIN(F) ((F) == 0 ? 16 : 1)
+#endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
 #endif
@@ -97,6 +102,9 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     for (;;) {
       unsigned long long idle = __ballot(!ps.active);
       if (idle == 0 || next_item >= n_items) break;
+      // refill only once enough lanes are idle: camera-ray generation costs the
+      // whole wave, however few lanes take new paths
+      if (__popcll(idle) < RT_REGEN_MIN(F) && ~idle != 0ull) break;
       int rank = __popcll(idle & ((1ull << lane) - 1ull));
       int item = next_item + rank;
       next_item += __popcll(idle);
