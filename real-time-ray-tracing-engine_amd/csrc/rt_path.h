@@ -122,7 +122,12 @@ enum : unsigned {
 };
 
 // ---------------------------------------------------------------- textures
-RT_HD double perlin_noise(const DPerlin &P, V3 p) { // PerlinNoise.hpp:43-60, 186-201
+// PerlinNoise::noise + perlin_interp (PerlinNoise.hpp:43-60, 186-201).  The
+// reference's corner weight i*uu + (1-i)*(1-uu) is uu or 1-uu and (u - i) is u or
+// u-1: the same doubles for every input (0*x + y == y, x - 0 == x here; NaN stays
+// NaN), without the dead multiplies.  Corner order and the ((fi*fj)*fk)*dot
+// grouping are the reference's.
+RT_HD double perlin_noise(const DPerlin &P, V3 p) {
   double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
   double u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int xi = (int)fx, yi = (int)fy, zi = (int)fz;
@@ -130,14 +135,14 @@ RT_HD double perlin_noise(const DPerlin &P, V3 p) { // PerlinNoise.hpp:43-60, 18
   double acc = 0.0;
   for (int i = 0; i < 2; i++) {
     int pxi = P.px[(xi + i) & 255];
-    double fi = i * uu + (1 - i) * (1 - uu);
+    double fi = i ? uu : 1 - uu, di = i ? u - 1 : u;
     for (int j = 0; j < 2; j++) {
       int pyj = P.py[(yi + j) & 255];
-      double fj = j * vv + (1 - j) * (1 - vv);
+      double fj = j ? vv : 1 - vv, dj = j ? v - 1 : v;
       for (int k = 0; k < 2; k++) {
         const double *g = P.rv[pxi ^ pyj ^ P.pz[(zi + k) & 255]];
-        V3 wv = v3(u - i, v - j, w - k);
-        acc += fi * fj * (k * ww + (1 - k) * (1 - ww)) * dot(ld3(g), wv);
+        double fk = k ? ww : 1 - ww, dk = k ? w - 1 : w;
+        acc += fi * fj * fk * (g[0] * di + g[1] * dj + g[2] * dk);
       }
     }
   }
