@@ -4,7 +4,7 @@
 set -e
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r01c
+O=$R/gpurun_out/${PASS:-r01c}
 mkdir -p $O
 cd $R
 timeout -k 10 400 python -m pytest tests -q -m gpu -x > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
