@@ -36,6 +36,7 @@
 #include "scene/textures/NoiseTexture.hpp"
 #include "scene/textures/SolidColorTexture.hpp"
 #include "utils/ColorUtility.hpp"
+#include "ref_binding.hpp"
 #include "utils/math/Utility.hpp"
 
 #include <atomic>
@@ -241,6 +242,20 @@ void root_lists(Graph &g, const rt_scene_desc *d, HittableList &world, HittableL
 } // namespace
 
 extern "C" {
+
+/* INTEGRATION.md's binding against the real classes: rebuild `d` as reference
+   objects, convert them back with RtSceneBuilder (ref_binding.hpp).  The tables
+   behind *out stay valid until the next call. */
+int ref_binding_roundtrip(const rt_scene_desc *d, rt_scene_desc *out) {
+  static std::unique_ptr<RtSceneBuilder> builder;
+  Graph g;
+  g.load(d);
+  HittableList world, lights;
+  root_lists(g, d, world, lights);
+  builder.reset(new RtSceneBuilder());
+  *out = builder->finish(world, lights, d->use_bvh != 0);
+  return 0;
+}
 
 int ref_camera_setup(const rt_camera_desc *cam, rt_frame *f) {
   GoldenCamera c(make_config(cam, false, false));

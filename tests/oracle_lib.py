@@ -112,6 +112,26 @@ def ref_render(scene, cam, seed, use_bvh=None):
     return out
 
 
+def ref_binding_roundtrip(scene):
+    """Scene -> reference objects -> INTEGRATION.md's binding (oracle/ref_binding.hpp)
+    -> a new SceneDescription built from the binding's tables."""
+    from rtx.scene import SceneDescription
+    d = scene.desc()
+    out = abi.SceneDesc()
+    L = ref()
+    L.ref_binding_roundtrip.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.SceneDesc)]
+    assert L.ref_binding_roundtrip(C.byref(d), C.byref(out)) == 0
+    R = SceneDescription()
+    R.textures = [abi.TextureDesc.from_buffer_copy(out.textures[k]) for k in range(out.n_textures)]
+    R.perlin = [abi.PerlinDesc.from_buffer_copy(out.perlin[k]) for k in range(out.n_perlin)]
+    R.materials = [abi.MaterialDesc.from_buffer_copy(out.materials[k]) for k in range(out.n_materials)]
+    R.objects = [abi.ObjectDesc.from_buffer_copy(out.objects[k]) for k in range(out.n_objects)]
+    R.children = [int(out.children[k]) for k in range(out.n_children)]
+    R.world, R.lights, R.use_bvh = out.world, out.lights, out.use_bvh
+    R.camera = scene.camera
+    return R
+
+
 def ref_trace_parallel(scene, cam, threads, use_bvh=None):
     """Reference code, -p decomposition over `threads` host threads (CPU baseline)."""
     d = scene.desc()
