@@ -33,6 +33,12 @@
  * builds its own acceleration structure and uploads a device layout that the
  * library owns.  The caller owns every pointer it passes in.
  *
+ * Threading.  Distinct rt_scene objects are independent and may be used from
+ * different host threads (and devices) at once.  One rt_scene is used by one
+ * host thread at a time: its kernel-timing events and its scratch / staging
+ * buffers are per scene.  Asynchronous launches (rt_render_device) on one
+ * scene must be ordered by the caller's streams as any device work is.
+ *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
  * random stream is a stateless counter-based Philox4x32-10 keyed by
  * (seed, pixel, stratum sample, bounce, slot); see DESIGN.md "RNG contract".

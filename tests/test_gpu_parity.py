@@ -185,3 +185,27 @@ def test_render_device_is_ordered_with_torch_stream():
             got = buf.cpu().numpy()  # syncs torch's stream only
         one = R.render(f, seed=5, output=abi.RT_OUT_SUM)
     np.testing.assert_allclose(got, 2 * one, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_two_scenes_render_concurrently_from_two_threads():
+    """Distinct rt_scene objects are independent (rt_api.h "Threading"): two host
+    threads render two scenes at once and each matches its own oracle."""
+    import threading
+    jobs = [("cornell", 32, 9, 3), ("bouncing_seed42", 40, 4, 8)]
+    out = {}
+
+    def run(name, w, spp, seed):
+        S = scene(name)
+        cam = S.camera_desc(image_width=w, samples_per_pixel=spp, max_depth=6)
+        with Renderer(S) as R:
+            for _ in range(3):
+                out[name] = (R.render(camera_frame(cam), seed=seed), S, cam, seed)
+
+    th = [threading.Thread(target=run, args=j) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for name, (img, S, cam, seed) in out.items():
+        compare(img, O.oracle_render(S, cam, O.MODE_COUNTER, seed))
