@@ -65,11 +65,11 @@ def algorithmic_bytes(st, info, n_pixels):
 def cpu_baseline(scene, cam_full, threads):
     """The reference's own C++ path (oracle/_ref, built from /root/reference/src)
     with its -p decomposition over `threads` host threads, on a bounded sample:
-    the full frame at 4x4 strata (same scene, depth, resolution; ~10 s)."""
+    the full frame at 5x5 strata (same scene, depth, resolution; ~15 s)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     from rtx.scene import camera_desc  # noqa: F401
-    spp = 16
+    spp = 25
     cam = scene.camera_desc(image_width=cam_full.image_width, samples_per_pixel=spp,
                             max_depth=cam_full.max_depth)
     if O.ref_available():
