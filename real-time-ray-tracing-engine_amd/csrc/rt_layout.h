@@ -54,7 +54,7 @@ struct DXform {      // 32 B — Translate offset or RotateY (sin, cos)
 struct DSphere {     // 64 B — Sphere.hpp: m_center Ray (c0, c1-c0), m_radius
   double c0[3];
   double dir[3];     // c1 - c0, 0 for static spheres
-  double r;
+  double inv_r;      // 1 / r: the reference's (p - c) / r is (1 / r) * (p - c) (Vec3.hpp:88)
   double rr;         // r*r, as Sphere::hit computes it
 };
 

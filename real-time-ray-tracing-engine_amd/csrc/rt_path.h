@@ -78,7 +78,6 @@ struct Hit {
 };
 
 // ---------------------------------------------------------------- RNG
-RT_HD RT_FI uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 struct Key {
   uint32_t k0, k1, pixel, sample;
 };
@@ -90,13 +89,14 @@ RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    // one 32x32->64 product per multiplier (v_mad_u64_u32), not a separate
+    // mul_hi + mul_lo pair: half the quarter-rate integer multiplies
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
     c0 = n0;
-    c1 = lo1;
+    c1 = (uint32_t)p1;
     c2 = n2;
-    c3 = lo0;
+    c3 = (uint32_t)p0;
   }
   out[0] = c0;
   out[1] = c1;
@@ -110,6 +110,42 @@ RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]
   philox10(k.pixel, k.sample, bounce, slot, k.k0, k.k1, x);
 #pragma unroll
   for (int q = 0; q < 4; ++q) u[q] = (double)x[q] * 0x1.0p-32;
+}
+
+// sin and cos of 2*pi*u for a uniform u = k * 2^-32 in [0, 1) (every angle the
+// path draws: disk, cosine, unit-vector and light-cone directions).  Quadrant
+// reduction in u is exact (4u and 4u - q are exact doubles), so no Cody-Waite or
+// Payne-Hanek reduction is needed; the kernels on [-pi/4, pi/4] are the
+// fdlibm/FreeBSD k_sin/k_cos minimax polynomials.  Max |error| 1.4e-16 against
+// the exact sin(2 pi u) (the reference's sin(fl(2 pi u)) is itself up to 4.4e-16
+// from it); tested in tests/test_emulator.py.
+#ifndef RT_SINCOS_2PI
+#define RT_SINCOS_2PI 1
+#endif
+RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
+#if RT_SINCOS_2PI
+  const double t = 4.0 * u;
+  const double q = floor(t + 0.5);
+  const double x = (t - q) * 1.5707963267948966;
+  const double z = x * x;
+  const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                      2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                        8.33333333332248946124e-03);
+  const double sn = fma(z * x, fma(z, ps, -1.66666666666666324348e-01), x);
+  const double pc =
+      z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                   -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                     -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cn = w + (((1.0 - w) - hz) + z * pc);
+  const int qi = (int)q & 3;
+  s = (qi & 1) ? cn : sn;
+  c = (qi & 1) ? sn : cn;
+  if (qi >= 2) s = -s;
+  if (qi == 1 || qi == 2) c = -c;
+#else
+  sincos(2.0 * kPi * u, &s, &c);
+#endif
 }
 
 // ---------------------------------------------------------------- features
@@ -202,7 +238,7 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
   V3 cc = v3(s.c0[0] + r.tm * s.dir[0], s.c0[1] + r.tm * s.dir[1], s.c0[2] + r.tm * s.dir[2]);
   h.t = t;
   h.p = at(r, t);
-  V3 on = (1 / s.r) * (h.p - cc);
+  V3 on = s.inv_r * (h.p - cc); // inv_r = 1 / r, the same double the reference forms
   h.front = dot(r.d, on) < 0;
   h.n = h.front ? on : -on;
   h.mat = mat;
@@ -434,7 +470,24 @@ RT_HD RT_FI float f32_dn(double x) { // largest float <= x (x not NaN)
   if ((double)f > x) f = (f == 0.0f) ? f32_from(0x80000001u) : f32_from(f > 0.0f ? f32_bits(f) - 1u : f32_bits(f) + 1u);
   return f;
 }
+// 1/d for the slab test in fp32: v_rcp_f32 (1 ulp) of the rounded direction,
+// instead of an fp64 division rounded to fp32 (relative error <= 2^-22.4 vs
+// 2^-24; the far-distance growth below still covers the slab error with room).
+#ifndef RT_RCP32
+#define RT_RCP32 1
+#endif
+RT_HD RT_FI float rcp32(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+#if RT_RCP32
+constexpr float kSlabGrow = 1.0f + 0x1p-19f;
+#else
 constexpr float kSlabGrow = 1.0f + 0x1p-20f;
+#endif
 constexpr float kInvClamp = 1e30f; // finite 1/d: a 0 * inf NaN would drop a box
 
 struct RayF { // per-ray fp32 slab-test constants
@@ -447,7 +500,11 @@ RT_HD RT_FI RayF ray_f32(const Ray &r) {
   for (int a = 0; a < 3; ++a) {
     q.oa[a] = f32_up(o[a]);
     q.ob[a] = f32_dn(o[a]);
+#if RT_RCP32
+    float iv = rcp32((float)d[a]);
+#else
     float iv = (float)(1.0 / d[a]);
+#endif
     q.inv[a] = fminf(fmaxf(iv, -kInvClamp), kInvClamp);
   }
   return q;
@@ -674,7 +731,7 @@ RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double 
     V3 uu = cross(w, vv);
     double z = 1 + r2 * (sqrt(1 - s.rr / d2) - 1);
     double sphi, cphi;
-    sincos(2 * kPi * r1, &sphi, &cphi);
+    sincos_2pi(r1, sphi, cphi);
     double x = cphi * sqrt(1 - z * z);
     double y = sphi * sqrt(1 - z * z);
     d = ((x * uu) + (y * vv)) + (z * w);
@@ -745,7 +802,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     double z = 1.0 - 2.0 * d0;
     double rr = sqrt(fmax(0.0, 1.0 - z * z));
     double sp, cp;
-    sincos(2.0 * kPi * d1, &sp, &cp);
+    sincos_2pi(d1, sp, cp);
     V3 uv = v3(rr * cp, rr * sp, z);
     refl = unitv(refl) + (M.fuzz * uv);
     ps.T = ps.T * ld3(M.albedo);
@@ -800,7 +857,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   if (!from_light) {
     if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
       double sp, cp;
-      sincos(2 * kPi * d0, &sp, &cp);
+      sincos_2pi(d0, sp, cp);
       double sr = sqrt(d1);
       V3 lc = v3(cp * sr, sp * sr, sqrt(1 - d1));
       gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
@@ -808,7 +865,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
       double z = 1.0 - 2.0 * d0;
       double rr = sqrt(fmax(0.0, 1.0 - z * z));
       double sp, cp;
-      sincos(2.0 * kPi * d1, &sp, &cp);
+      sincos_2pi(d1, sp, cp);
       gd = v3(rr * cp, rr * sp, z);
     }
   }
@@ -858,7 +915,7 @@ RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k
     const double a = dk[0], b = dk[1];
     double rr = sqrt(a);
     double s, c;
-    sincos(2.0 * kPi * b, &s, &c);
+    sincos_2pi(b, s, c);
     double dx = rr * c, dy = rr * s;
     org = (org + (dx * ld3(C.disk_u))) + (dy * ld3(C.disk_v)); // Camera.cpp:226-230
   }

@@ -514,8 +514,9 @@ struct Compiler {
     P3 dir = sphere_dir(x);
     s.c0[0] = c0.x, s.c0[1] = c0.y, s.c0[2] = c0.z;
     s.dir[0] = dir.x, s.dir[1] = dir.y, s.dir[2] = dir.z;
-    s.r = std::fmax(0, x.s);
-    s.rr = s.r * s.r;
+    const double r = std::fmax(0, x.s);
+    s.inv_r = 1 / r;
+    s.rr = r * r;
     sphere_of[o] = (int)H.spheres.size();
     H.spheres.push_back(s);
     return sphere_of[o];

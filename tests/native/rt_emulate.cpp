@@ -116,3 +116,8 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
     }
   return 0;
 }
+
+// sincos_2pi over n uniforms (its accuracy test, tests/test_emulator.py)
+extern "C" void emu_sincos_2pi(const double *u, int n, double *s, double *c) {
+  for (int k = 0; k < n; ++k) rtp::sincos_2pi(u[k], s[k], c[k]);
+}
