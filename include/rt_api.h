@@ -245,6 +245,13 @@ typedef struct rt_path_stats {
   uint64_t other_tests;    /* instance / medium / list object visits */
   uint64_t light_tests;    /* primitive tests done by light pdf_value */
   uint64_t shade_events;   /* material evaluations */
+  /* SIMD efficiency: iterations summed over wavefronts (each iteration occupies
+     64 lane slots; e.g. node_visits / (64 * wave_node_iters) is the fraction of
+     lanes doing useful node work) */
+  uint64_t wave_trips;      /* path-loop trips (one segment attempt per lane) */
+  uint64_t wave_node_iters; /* traversal node-loop iterations */
+  uint64_t wave_leaf_iters; /* leaf-item loop iterations */
+  uint64_t wave_shade_iters; /* shading branch executions (lambertian/metal/dielectric/light) */
 } rt_path_stats;
 
 typedef struct rt_scene_info {

@@ -254,7 +254,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   size_t iTx = add(H.texs.data(), H.texs.size() * sizeof(DTex));
   size_t iP = add(H.perlin.data(), H.perlin.size() * sizeof(DPerlin));
   size_t iLi = add(H.lights.data(), H.lights.size() * sizeof(DLight));
-  size_t iSt = add(nullptr, 8 * sizeof(unsigned long long));
+  size_t iSt = add(nullptr, RT_N_STATS * sizeof(unsigned long long));
 
   rt_scene *s = new rt_scene();
   s->device = device;
@@ -509,10 +509,10 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   L.accumulate = 0;
   size_t n = out_doubles(f, L);
   if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
-  hipError_t e = hipMemsetAsync(s->stats, 0, 8 * sizeof(unsigned long long), s->stream);
+  hipError_t e = hipMemsetAsync(s->stats, 0, RT_N_STATS * sizeof(unsigned long long), s->stream);
   if (e != hipSuccess) return hip_err(e, "hipMemsetAsync stats");
   if ((rc = launch(s, C, L, s->out_buf, s->stats, s->stream))) return rc;
-  unsigned long long h[8];
+  unsigned long long h[RT_N_STATS];
   e = hipMemcpyAsync(h, s->stats, sizeof h, hipMemcpyDeviceToHost, s->stream);
   if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync stats");
   e = hipStreamSynchronize(s->stream);
@@ -525,6 +525,10 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->other_tests = h[5];
   stats->light_tests = h[6];
   stats->shade_events = h[7];
+  stats->wave_trips = h[8];
+  stats->wave_node_iters = h[9];
+  stats->wave_leaf_iters = h[10];
+  stats->wave_shade_iters = h[11];
   return RT_OK;
 }
 

@@ -88,8 +88,8 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   acc[lane * 3 + 1] = 0.0;
   acc[lane * 3 + 2] = 0.0;
 
-  Counters cnt{0, 0, 0, 0, 0, 0};
-  uint32_t n_samples = 0, n_segments = 0;
+  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
 
   const int n_items = 64 * max(0, s_count);
   int next_item = 0; // wave-uniform head of the tile's work queue
@@ -125,6 +125,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
       }
     }
     if (__ballot(ps.active) == 0) break;
+    if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
       if (STATS) n_segments++;
       bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt);
@@ -162,9 +163,10 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     }
   }
   if (STATS) {
-    unsigned long long v[8] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
-                               cnt.quads, cnt.other,  cnt.light, cnt.shade};
-    for (int k = 0; k < 8; ++k) {
+    unsigned long long v[RT_N_STATS] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
+                                        cnt.quads, cnt.other,  cnt.light, cnt.shade,
+                                        lane == 0 ? n_trips : 0u, cnt.wnode, cnt.wleaf, cnt.wshade};
+    for (int k = 0; k < RT_N_STATS; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
       if (lane == 0) atomicAdd(&stats[k], x);

@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
+#define RT_N_STATS 12      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 
 enum DItemKind {

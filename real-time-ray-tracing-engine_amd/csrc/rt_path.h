@@ -521,7 +521,24 @@ RT_HD RT_FI float slab(const RayF &q, const float *lo, const float *hi, float tm
 
 struct Counters {
   uint32_t nodes, spheres, quads, other, light, shade;
+  uint32_t wnode, wleaf, wshade; // wave-level iterations (counted by one lane per wave)
 };
+// true when no active lane of the wavefront has `pred` (a single-lane host build: !pred)
+RT_HD RT_FI bool wave_none(bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(pred) == 0;
+#else
+  return !pred;
+#endif
+}
+// STATS only: 1 on the first active lane of the wavefront, else 0 (wave-level counts)
+RT_HD RT_FI uint32_t wave_once() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)(__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()));
+#else
+  return 1u;
+#endif
+}
 
 // Stack entry: >= 0 inner node; < 0 a leaf ~(first << 3 | count) (DNode::entry).
 
@@ -542,31 +559,28 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   const float tmin32 = f32_dn(tmin);
   float cl32 = __builtin_huge_valf(); // f32_up(closest)
 
+  // Speculative while-while traversal (Aila & Laine 2009, "postponed leaves"):
+  // a lane that reaches its first leaf parks it in (lf, ln) and keeps walking
+  // its stack; the wave leaves the node loop only once every lane still walking
+  // holds a leaf (or has finished), so node-loop slots that lanes with a leaf
+  // would otherwise idle through do useful visits.  Stack pops happen eagerly
+  // inside the visiting iteration (no separate pop iterations).  Entries: >= 0
+  // inner node, -1 none (stack empty: done after the parked leaf), <= -2 a leaf
+  // ~(first << 3 | count) (count >= 1).  Visiting order only changes how much
+  // the closest-hit bound culls, never the closest hit.
   int sp = 0;
-  int cur;   // current entry: node (>= 0) or leaf (< 0)
+  int cur;
   int lf = 0, ln = 0;
   if (S.root_is_leaf) {
     cur = -1;
-    lf = 0;
     ln = S.n_root_items;
   } else {
     cur = 0;
   }
-  // while-while traversal (Aila & Laine 2009): every lane descends until it
-  // holds a leaf (or runs out of work), then the wave tests leaf items together.
   for (;;) {
-    while (ln == 0) {
-      if (cur < 0) {
-        if (sp == 0) break;
-        cur = stk[64 * --sp];
-        if (cur < 0) {
-          lf = (~cur) >> 3;
-          ln = (~cur) & 7;
-          cur = -1;
-        }
-        continue;
-      }
-      // ---- inner node: test both children's boxes
+    while (cur >= 0) {
+      if (STATS) cnt.wnode += wave_once();
+      if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them
       if (STATS) cnt.nodes++;
       DNode N;
       if (cur < S.n_lds_nodes) {
@@ -588,25 +602,23 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       const int e0 = N.entry[0], e1 = N.entry[1];
       const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
       if (h0 && h1) {
-        bool first0 = tn0 <= tn1;
+        const bool first0 = tn0 <= tn1;
         if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
         cur = first0 ? e0 : e1;
-      } else if (h0) {
-        cur = e0;
-      } else if (h1) {
-        cur = e1;
+      } else if (h0 || h1) {
+        cur = h0 ? e0 : e1;
       } else {
-        cur = -1;
-        continue;
+        cur = sp > 0 ? stk[64 * --sp] : -1;
       }
-      if (cur < 0) {
+      if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
         lf = (~cur) >> 3;
         ln = (~cur) & 7;
-        cur = -1;
+        cur = sp > 0 ? stk[64 * --sp] : -1;
       }
     }
-    if (ln == 0) break; // stack empty and no pending leaf: done
+    if (ln == 0) break; // nothing parked and nothing left to walk: done
     while (ln > 0) { // ---- the single leaf-test site
+      if (STATS) cnt.wleaf += wave_once();
       const int ii = lf;
       ++lf;
       --ln;
@@ -634,6 +646,11 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         best = ii;
         best_full = false;
       }
+    }
+    if (cur < -1) { // a second leaf met while one was parked: it is next
+      lf = (~cur) >> 3;
+      ln = (~cur) & 7;
+      cur = sp > 0 ? stk[64 * --sp] : -1;
     }
   }
   // Media after the BVH walk, against the final primitive distance: the closest
@@ -787,6 +804,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   const DMat M = S.mats[h.mat];
   if (STATS) cnt.shade++;
   if (M.kind == RT_MAT_DIFFUSE_LIGHT) { // emits on the front face, never scatters
+    if (STATS) cnt.wshade += wave_once();
     // Always add T * emitted (0 on the back face): a NaN/inf throughput must
     // poison the sample as the reference recursion does (NaN * 0 = NaN).
     V3 e = h.front ? tex_value<F>(S, M.tex, h.p) : v3(0.0, 0.0, 0.0);
@@ -798,6 +816,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   if (M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
+    if (STATS) cnt.wshade += wave_once();
     V3 refl = r.d - (2 * dot(r.d, h.n)) * h.n;
     double z = 1.0 - 2.0 * d0;
     double rr = sqrt(fmax(0.0, 1.0 - z * z));
@@ -810,6 +829,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     return advance(ps, C);
   }
   if (M.kind == RT_MAT_DIELECTRIC) { // DielectricMaterial.cpp:58-85
+    if (STATS) cnt.wshade += wave_once();
     double ri = h.front ? (1.0 / M.ior) : M.ior;
     V3 ud = unitv(r.d);
     double ct = fmin(dot(-ud, h.n), 1.0);
@@ -836,6 +856,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   }
   // Lambertian (CosinePDF) or Isotropic (SpherePDF), mixed 50/50 with the lights
   const bool lamb = (M.kind == RT_MAT_LAMBERTIAN);
+  if (STATS) cnt.wshade += wave_once();
   // albedo: fetched early when a noise texture may run (its long evaluation
   // overlaps less live state there), late otherwise (shorter live range)
   V3 att;

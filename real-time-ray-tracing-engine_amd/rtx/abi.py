@@ -98,7 +98,8 @@ RT_LAYOUT_FRAME, RT_LAYOUT_TILES = 0, 1
 class PathStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "samples", "segments", "node_visits", "sphere_tests", "quad_tests",
-        "other_tests", "light_tests", "shade_events")]
+        "other_tests", "light_tests", "shade_events",
+        "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters")]
 
 
 class SceneInfo(C.Structure):
