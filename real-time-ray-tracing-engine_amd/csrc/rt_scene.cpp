@@ -126,7 +126,11 @@ struct SahBuilder {
     int id = (int)bn.size();
     bn.push_back(n);
     const int kLeafMax = 2;
-    if (cnt <= kLeafMax) {
+    // A small world is one flat leaf (the reference's own HittableList walk,
+    // in list order): a wavefront's lanes scatter over the whole scene, so a
+    // split of a handful of items only adds a node visit and divergent leaf
+    // loops (C2: 3.2 wave leaf iterations + 1 node per segment vs 3 flat tests).
+    if (cnt <= kLeafMax || (dep == 0 && cnt <= RT_FLAT_MAX)) {
       bn[id].first = st;
       bn[id].count = cnt;
       return id;
