@@ -299,6 +299,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   d.n_nodes = (int32_t)H.nodes.size();
   d.root_is_leaf = H.root_is_leaf;
   d.n_root_items = H.n_root_items;
+  d.static_spheres = rtx::all_spheres_static(H);
   d.features = 0;
   if (!H.mitems.empty()) d.features |= RT_FEAT_MEDIA;
   for (const DItem &it : H.items)
@@ -343,6 +344,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     d.root_is_leaf = H.root_is_leaf;
     d.n_root_items = H.n_root_items;
   }
+  if (d.root_is_leaf) d.features |= RT_FEAT_FLAT;
   // traversal stack: one entry per BVH level suffices (a pushed entry is the
   // sibling of a node on the current root path); LDS prefix of the BFS-ordered
   // nodes sized to what the instance's occupancy leaves free

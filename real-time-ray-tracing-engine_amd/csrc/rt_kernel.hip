@@ -28,6 +28,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
+#include <utility>
+
 #include "rt_path.h"
 
 namespace {
@@ -36,7 +39,7 @@ using namespace rtp;
 // Idle lanes that trigger a refill while other lanes still trace (measured:
 // 16 for the plain instance, C3 +4 %; the rich instances lose with any delay).
 #ifndef RT_REGEN_MIN
-#define RT_REGEN_MIN(F) ((F) == 0 ? 16 : 1)
+#define RT_REGEN_MIN(F) (((F) & ~F_FLAT) == 0 ? 16 : 1)
 #endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
@@ -52,7 +55,7 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_WAVES_OTHER
 #define RT_WAVES_OTHER 3
 #endif
-#define RT_WAVES_PER_EU(F) ((F) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER)
+#define RT_WAVES_PER_EU(F) (((F) & ~F_FLAT) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER)
 
 template <bool STATS, unsigned F>
 __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
           ps.sample = s_first + (item >> 6);
           key.pixel = (uint32_t)(j * C.W + i);
           key.sample = (uint32_t)ps.sample;
-          ps.ray = camera_ray(C, key, i, j, ps.sample);
+          ps.ray = camera_ray<F == F_FLAT>(C, key, i, j, ps.sample);
           ps.T = v3(1.0, 1.0, 1.0);
           ps.bounce = 0;
           ps.active = C.max_depth > 0;
@@ -205,22 +208,16 @@ __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint
 
 using RenderFn = void (*)(DScene, DCamera, DLaunch, double *, unsigned long long *);
 
+template <bool STATS, unsigned... Fs>
+constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequence<unsigned, Fs...>) {
+  return {render_tiles<STATS, Fs>...};
+}
+
+// one instance per feature set (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE | F_FLAT)
 const RenderFn *render_table(bool stats) {
-  static constexpr RenderFn plain[16] = {
-      render_tiles<false, 0>,  render_tiles<false, 1>,  render_tiles<false, 2>,
-      render_tiles<false, 3>,  render_tiles<false, 4>,  render_tiles<false, 5>,
-      render_tiles<false, 6>,  render_tiles<false, 7>,  render_tiles<false, 8>,
-      render_tiles<false, 9>,  render_tiles<false, 10>, render_tiles<false, 11>,
-      render_tiles<false, 12>, render_tiles<false, 13>, render_tiles<false, 14>,
-      render_tiles<false, 15>};
-  static constexpr RenderFn counted[16] = {
-      render_tiles<true, 0>,  render_tiles<true, 1>,  render_tiles<true, 2>,
-      render_tiles<true, 3>,  render_tiles<true, 4>,  render_tiles<true, 5>,
-      render_tiles<true, 6>,  render_tiles<true, 7>,  render_tiles<true, 8>,
-      render_tiles<true, 9>,  render_tiles<true, 10>, render_tiles<true, 11>,
-      render_tiles<true, 12>, render_tiles<true, 13>, render_tiles<true, 14>,
-      render_tiles<true, 15>};
-  return stats ? counted : plain;
+  static constexpr auto plain = instance_table<false>(std::make_integer_sequence<unsigned, F_ALL + 1>{});
+  static constexpr auto counted = instance_table<true>(std::make_integer_sequence<unsigned, F_ALL + 1>{});
+  return stats ? counted.data() : plain.data();
 }
 
 } // namespace

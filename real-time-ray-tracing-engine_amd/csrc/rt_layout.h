@@ -135,6 +135,7 @@ struct DScene {      // kernel argument (by value)
   int32_t n_mitems;
   int32_t stack_depth;   // per-lane traversal stack entries (BVH depth + 1)
   int32_t n_lds_nodes;   // nodes [0, n_lds_nodes) are staged in LDS (BFS order: top levels)
+  int32_t static_spheres; // 1: every sphere has c1 == c0 (no motion blur): center = c0
 };
 
 // Scene features (kernel specialisation keys)
@@ -142,6 +143,7 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_XFORM 2  // transform chains on world items or lights
 #define RT_FEAT_LIGHTS 4 // non-empty light list
 #define RT_FEAT_NOISE 8  // Perlin noise textures
+#define RT_FEAT_FLAT 16  // flat world (root_is_leaf): no BVH walk
 
 struct DCamera {     // the rt_frame values the kernel needs
   double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];

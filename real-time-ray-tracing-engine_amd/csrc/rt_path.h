@@ -81,8 +81,18 @@ struct Hit {
 struct Key {
   uint32_t k0, k1, pixel, sample;
 };
+// KB ("key barrier"): hide the wave-uniform key from the optimiser at entry,
+// so the round keys are re-derived with scalar adds in every call.  Without it
+// the 20 round keys are hoisted out of the path loop, spill to VGPR lanes and
+// cost a v_readlane (plus hazard nops) per use.  Measured per instance: the
+// plain flat instance gains (C2 +3 %); the rich instances lose badly (C4 -25 %,
+// more SGPR pressure there), so only the former sets it.
+template <bool KB = false>
 RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                          uint32_t k0, uint32_t k1, uint32_t out[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KB) asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
@@ -105,9 +115,10 @@ RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
 }
 // Four uniforms in [0,1) (x * 2^-32, exact in fp64) from one Philox block for
 // (bounce, slot) — DESIGN.md "RNG contract".
+template <bool KB = false>
 RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]) {
   uint32_t x[4];
-  philox10(k.pixel, k.sample, bounce, slot, k.k0, k.k1, x);
+  philox10<KB>(k.pixel, k.sample, bounce, slot, k.k0, k.k1, x);
 #pragma unroll
   for (int q = 0; q < 4; ++q) u[q] = (double)x[q] * 0x1.0p-32;
 }
@@ -154,7 +165,8 @@ enum : unsigned {
   F_XFORM = 2u,  // RotateY/Translate chains on world items or lights
   F_LIGHTS = 4u, // a non-empty light list (mixture with light sampling)
   F_NOISE = 8u,  // Perlin noise textures
-  F_ALL = 15u
+  F_FLAT = 16u,  // flat world (root_is_leaf): every item tested in list order, no BVH walk
+  F_ALL = 31u
 };
 
 // ---------------------------------------------------------------- textures
@@ -216,9 +228,16 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
 
 // ------------------------------------------------------------ primitives
 // Sphere::hit root search (Sphere.cpp:101-127).
+// The center at the ray's time, center.at(time) = c0 + tm * (c1 - c0): exactly
+// c0 for a static sphere (dir = 0), so scenes without motion skip the six ops
+// (DScene::static_spheres, wave-uniform).
+RT_HD RT_FI V3 sphere_center(const DSphere &s, double tm, bool moving) {
+  if (!moving) return ld3(s.c0);
+  return v3(s.c0[0] + tm * s.dir[0], s.c0[1] + tm * s.dir[1], s.c0[2] + tm * s.dir[2]);
+}
 RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tmin,
-                                            double tmax, double &root) {
-  V3 cc = v3(s.c0[0] + r.tm * s.dir[0], s.c0[1] + r.tm * s.dir[1], s.c0[2] + r.tm * s.dir[2]);
+                                            double tmax, double &root, bool moving = true) {
+  V3 cc = sphere_center(s, r.tm, moving);
   V3 oc = cc - r.o;
   double h = dot(r.d, oc);
   double c = len2(oc) - s.rr;
@@ -234,8 +253,8 @@ RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tm
   return true;
 }
 RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat,
-                                              Hit &h) {
-  V3 cc = v3(s.c0[0] + r.tm * s.dir[0], s.c0[1] + r.tm * s.dir[1], s.c0[2] + r.tm * s.dir[2]);
+                                              Hit &h, bool moving = true) {
+  V3 cc = sphere_center(s, r.tm, moving);
   h.t = t;
   h.p = at(r, t);
   V3 on = s.inv_r * (h.p - cc); // inv_r = 1 / r, the same double the reference forms
@@ -555,102 +574,121 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   int best = -1;
   bool best_full = false;
   const double a = len2(r.d);
-  const RayF q = ray_f32(r);
-  const float tmin32 = f32_dn(tmin);
+  // F_FLAT instances (small worlds, SAH root is one leaf) have no BVH walk; they
+  // need the fp32 slab constants only for the medium box cull, and they skip
+  // the center.at(time) arithmetic when no sphere moves (a wave-uniform flag).
+  constexpr bool kFlat = (F & F_FLAT) != 0;
+  constexpr bool kBoxes = !kFlat || (F & F_MEDIA) != 0;
+  const bool moving = kFlat ? !S.static_spheres : true;
+  RayF q{};
+  float tmin32 = 0.0f;
   float cl32 = __builtin_huge_valf(); // f32_up(closest)
-
-  // Speculative while-while traversal (Aila & Laine 2009, "postponed leaves"):
-  // a lane that reaches its first leaf parks it in (lf, ln) and keeps walking
-  // its stack; the wave leaves the node loop only once every lane still walking
-  // holds a leaf (or has finished), so node-loop slots that lanes with a leaf
-  // would otherwise idle through do useful visits.  Stack pops happen eagerly
-  // inside the visiting iteration (no separate pop iterations).  Entries: >= 0
-  // inner node, -1 none (stack empty: done after the parked leaf), <= -2 a leaf
-  // ~(first << 3 | count) (count >= 1).  Visiting order only changes how much
-  // the closest-hit bound culls, never the closest hit.
-  int sp = 0;
-  int cur;
-  int lf = 0, ln = 0;
-  if (S.root_is_leaf) {
-    cur = -1;
-    ln = S.n_root_items;
-  } else {
-    cur = 0;
+  if constexpr (kBoxes) {
+    q = ray_f32(r);
+    tmin32 = f32_dn(tmin);
   }
-  for (;;) {
-    while (cur >= 0) {
-      if (STATS) cnt.wnode += wave_once();
-      if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them
-      if (STATS) cnt.nodes++;
-      DNode N;
-      if (cur < S.n_lds_nodes) {
-        const RT_LDS DNode &L = lnodes[cur];
+  // closest-hit test of one world item (records only t and the item index)
+  auto test_item = [&](int ii) {
+    if (STATS) cnt.wleaf += wave_once();
+    const DItem it = S.items[ii];
+    Ray lr = r;
+    double al = a;
+    if constexpr ((F & F_XFORM) != 0) {
+      if (it.xf_count) {
+        lr = to_local(S, it.xf_first, it.xf_count, r);
+        al = len2(lr.d);
+      }
+    }
+    double t;
+    bool hit;
+    if (it.kind == I_SPHERE) {
+      if (STATS) cnt.spheres++;
+      hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t, moving);
+    } else {
+      if (STATS) cnt.quads++;
+      hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
+    }
+    if (hit) {
+      closest = t;
+      if constexpr (kBoxes) cl32 = f32_up(closest);
+      best = ii;
+      best_full = false;
+    }
+  };
+
+  if constexpr (kFlat) {
+    // the reference's HittableList walk (HittableList.cpp), wave-uniform items
+    for (int ii = 0; ii < S.n_root_items; ++ii) test_item(ii);
+  } else {
+    // Speculative while-while traversal (Aila & Laine 2009, "postponed leaves"):
+    // a lane that reaches its first leaf parks it in (lf, ln) and keeps walking
+    // its stack; the wave leaves the node loop only once every lane still walking
+    // holds a leaf (or has finished), so node-loop slots that lanes with a leaf
+    // would otherwise idle through do useful visits.  Stack pops happen eagerly
+    // inside the visiting iteration (no separate pop iterations).  Entries: >= 0
+    // inner node, -1 none (stack empty: done after the parked leaf), <= -2 a leaf
+    // ~(first << 3 | count) (count >= 1).  Visiting order only changes how much
+    // the closest-hit bound culls, never the closest hit.
+    int sp = 0;
+    int cur;
+    int lf = 0, ln = 0;
+    if (S.root_is_leaf) {
+      cur = -1;
+      ln = S.n_root_items;
+    } else {
+      cur = 0;
+    }
+    for (;;) {
+      while (cur >= 0) {
+        if (STATS) cnt.wnode += wave_once();
+        if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them
+        if (STATS) cnt.nodes++;
+        DNode N;
+        if (cur < S.n_lds_nodes) {
+          const RT_LDS DNode &L = lnodes[cur];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          N.lo0[k] = L.lo0[k];
-          N.hi0[k] = L.hi0[k];
-          N.lo1[k] = L.lo1[k];
-          N.hi1[k] = L.hi1[k];
+          for (int k = 0; k < 3; ++k) {
+            N.lo0[k] = L.lo0[k];
+            N.hi0[k] = L.hi0[k];
+            N.lo1[k] = L.lo1[k];
+            N.hi1[k] = L.hi1[k];
+          }
+          N.entry[0] = L.entry[0];
+          N.entry[1] = L.entry[1];
+        } else {
+          N = S.nodes[cur];
         }
-        N.entry[0] = L.entry[0];
-        N.entry[1] = L.entry[1];
-      } else {
-        N = S.nodes[cur];
+        const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
+        const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
+        const int e0 = N.entry[0], e1 = N.entry[1];
+        const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
+        if (h0 && h1) {
+          const bool first0 = tn0 <= tn1;
+          if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
+          cur = first0 ? e0 : e1;
+        } else if (h0 || h1) {
+          cur = h0 ? e0 : e1;
+        } else {
+          cur = sp > 0 ? stk[64 * --sp] : -1;
+        }
+        if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
+          lf = (~cur) >> 3;
+          ln = (~cur) & 7;
+          cur = sp > 0 ? stk[64 * --sp] : -1;
+        }
       }
-      const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
-      const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
-      const int e0 = N.entry[0], e1 = N.entry[1];
-      const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
-      if (h0 && h1) {
-        const bool first0 = tn0 <= tn1;
-        if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
-        cur = first0 ? e0 : e1;
-      } else if (h0 || h1) {
-        cur = h0 ? e0 : e1;
-      } else {
-        cur = sp > 0 ? stk[64 * --sp] : -1;
+      if (ln == 0) break; // nothing parked and nothing left to walk: done
+      while (ln > 0) { // ---- the single leaf-test site
+        const int ii = lf;
+        ++lf;
+        --ln;
+        test_item(ii);
       }
-      if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
+      if (cur < -1) { // a second leaf met while one was parked: it is next
         lf = (~cur) >> 3;
         ln = (~cur) & 7;
         cur = sp > 0 ? stk[64 * --sp] : -1;
       }
-    }
-    if (ln == 0) break; // nothing parked and nothing left to walk: done
-    while (ln > 0) { // ---- the single leaf-test site
-      if (STATS) cnt.wleaf += wave_once();
-      const int ii = lf;
-      ++lf;
-      --ln;
-      const DItem it = S.items[ii];
-      Ray lr = r;
-      double al = a;
-      if constexpr ((F & F_XFORM) != 0) {
-        if (it.xf_count) {
-          lr = to_local(S, it.xf_first, it.xf_count, r);
-          al = len2(lr.d);
-        }
-      }
-      double t;
-      bool hit;
-      if (it.kind == I_SPHERE) {
-        if (STATS) cnt.spheres++;
-        hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t);
-      } else {
-        if (STATS) cnt.quads++;
-        hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
-      }
-      if (hit) {
-        closest = t;
-        cl32 = f32_up(closest);
-        best = ii;
-        best_full = false;
-      }
-    }
-    if (cur < -1) { // a second leaf met while one was parked: it is next
-      lf = (~cur) >> 3;
-      ln = (~cur) & 7;
-      cur = sp > 0 ? stk[64 * --sp] : -1;
     }
   }
   // Media after the BVH walk, against the final primitive distance: the closest
@@ -680,7 +718,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       if (it.xf_count) lr = to_local(S, it.xf_first, it.xf_count, r);
     }
     if (it.kind == I_SPHERE)
-      sphere_record(S.spheres[it.idx], lr, closest, it.mat, h);
+      sphere_record(S.spheres[it.idx], lr, closest, it.mat, h, moving);
     else
       quad_record(S.quads[it.idx], lr, closest, it.mat, h);
     if constexpr ((F & F_XFORM) != 0) {
@@ -812,7 +850,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     return false;
   }
   double rn[4]; // one block per shading event: (e0, e1, d0, d1)
-  u01x4(key, b, kSlotShade, rn);
+  u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   if (M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
@@ -920,11 +958,12 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   return advance(ps, C);
 }
 
+template <bool KB = false> // KB: philox10
 RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
   double rs = 1.0 / C.sqrt_spp;
   double jt[4]; // slot 0: jitter x, jitter y, time
-  u01x4(key, kCamTag, 0, jt);
+  u01x4<KB>(key, kCamTag, 0, jt);
   const double ja = jt[0], jb = jt[1];
   double px = ((si + ja) * rs) - 0.5;
   double py = ((sj + jb) * rs) - 0.5;
@@ -932,7 +971,7 @@ RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k
   V3 org = ld3(C.center);
   if (!(C.defocus_angle <= 0)) {
     double dk[4]; // slot 1: defocus disk (r^2, angle)
-    u01x4(key, kCamTag, 1, dk);
+    u01x4<KB>(key, kCamTag, 1, dk);
     const double a = dk[0], b = dk[1];
     double rr = sqrt(a);
     double s, c;

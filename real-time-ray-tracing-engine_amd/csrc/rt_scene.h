@@ -33,6 +33,14 @@ struct HostScene {
   double scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
 };
 
+// 1 when no sphere moves (DScene::static_spheres): the kernel then skips the
+// center.at(time) arithmetic, whose result is c0 exactly for these spheres.
+inline int32_t all_spheres_static(const HostScene &H) {
+  for (const DSphere &s : H.spheres)
+    if (s.dir[0] != 0.0 || s.dir[1] != 0.0 || s.dir[2] != 0.0) return 0;
+  return 1;
+}
+
 // Scenes with at least this many world primitives build their BVH on the
 // device when rt_scene_desc.bvh_builder is RT_BVH_AUTO.
 constexpr int kDeviceBuildMin = 65536;
