@@ -39,7 +39,10 @@ using namespace rtp;
 // Idle lanes that trigger a refill while other lanes still trace (measured:
 // 16 for the plain instance, C3 +4 %; the rich instances lose with any delay).
 #ifndef RT_REGEN_MIN
-#define RT_REGEN_MIN(F) (((F) & ~F_FLAT) == 0 ? 16 : 1)
+#ifndef RT_REGEN_FLAT
+#define RT_REGEN_FLAT 16
+#endif
+#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : ((F) == 0 ? 16 : 1))
 #endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
@@ -55,7 +58,10 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_WAVES_OTHER
 #define RT_WAVES_OTHER 3
 #endif
-#define RT_WAVES_PER_EU(F) (((F) & ~F_FLAT) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER)
+#ifndef RT_WAVES_FLAT
+#define RT_WAVES_FLAT 4
+#endif
+#define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : ((F) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 
 template <bool STATS, unsigned F>
 __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
