@@ -5,14 +5,17 @@
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
 
 A step renders one full frame of the workload (every pixel x every stratum x up
-to 8 bounces).  With N ranks the frame's strata are split into N disjoint ranges
-(one per GPU, all pixels each), every rank accumulates raw fp64 sums on its own
-device, and an RCCL reduce(sum) over xGMI combines them on rank 0 — the exchange
-step of the multi-GPU path (strong scaling: the frame is fixed, N varies).
+to 8 bounces).  With N ranks (default --shard tiles) tile t of the frame is
+rendered by rank t % N in stratum-chunked work units and one RCCL gather over
+xGMI brings the compact tile sums to rank 0; --shard strata splits the strata
+instead and combines full-frame sums with an RCCL reduce(sum).  Strong scaling:
+the frame is fixed, N varies.
 
 Output: ONE JSON line on rank 0 (driver contract) with a roofline object (the
-render kernel's algorithmic bytes / HIP-event duration vs HBM peak) and a CPU
-baseline (the reference's own code on the host cores, bounded sample).
+render kernel's algorithmic bytes / HIP-event duration vs HBM peak), a "valu"
+object (the kernel's real ceiling: fp64 FLOP/s and VALU issue occupancy from the
+committed PMC pass, profiles/pmc_<config>.json) and a CPU baseline (the
+reference's own code on the host cores, bounded sample).
 """
 import argparse
 import json
@@ -27,6 +30,7 @@ sys.path.insert(0, PKG)
 BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 SCENES = os.path.join(PKG, "scenes")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+F64_PEAK_TFS = 78.6    # MI355X fp64 vector peak (AMD spec): 16 FMA lanes/clk/SIMD at 2.4 GHz
 
 # BASELINE.json configs
 CONFIGS = {
@@ -264,12 +268,28 @@ def main():
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
+    pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(pmc_path))
+            traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            pmc = {}
+    valu = None
+    if pmc.get("f64_flops_per_launch") and ws == 1:
+        # fp64 work per launch is a property of the workload (PMC pass on the same
+        # command); divided by this run's live HIP-event kernel time
+        tfs = pmc["f64_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
+        valu = {"bound": "valu_f64", "achieved": round(tfs, 3), "peak": F64_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(tfs / F64_PEAK_TFS, 4),
+                "valu_busy": pmc.get("valu_busy"),
+                "valu_insts_per_launch": pmc.get("valu_insts_per_launch"),
+                "f64_insts_per_launch": pmc.get("f64_insts_per_launch"),
+                "note": "f64 FLOP = 64 x (ADD+MUL+TRANS) + 128 x FMA wave-instructions "
+                        "(PMC, every lane counted); valu_busy = SQ_ACTIVE_INST_VALU x 4 / "
+                        "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the share of SIMD cycles "
+                        "issuing VALU — the bound this kernel runs against"}
 
     out = {
         "metric": BASELINE["metric"],
@@ -303,6 +323,8 @@ def main():
                      "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
                      "counters": st},
     }
+    if valu is not None:
+        out["valu"] = valu
     if check is not None:
         out["check"] = check
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

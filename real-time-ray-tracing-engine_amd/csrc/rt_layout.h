@@ -87,10 +87,21 @@ struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + li
 
 struct DMat {        // 48 B
   int32_t kind, tex;
-  double albedo[3];
-  double fuzz;
+  union {
+    struct {         // lambertian / metal / isotropic / diffuse light
+      double albedo[3];
+      double fuzz;
+    };
+    struct {         // dielectric: constants formed once on the host with the
+                     // kernel's own operations (DielectricMaterial.cpp:62-66, 26-31):
+      double inv_ior; // 1/ior (the front-face ratio)
+      double r0[2];   // Schlick's ((1 - ri) / (1 + ri))^2 for ri = 1/ior (front), ior (back)
+      double pad_;
+    };
+  };
   double ior;
 };
+static_assert(sizeof(DMat) == 48, "DMat layout");
 
 struct DTex {        // 48 B
   int32_t kind, even, odd, perlin;

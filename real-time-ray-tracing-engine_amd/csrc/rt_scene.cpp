@@ -663,9 +663,18 @@ struct Compiler {
       std::memset(&d, 0, sizeof d);
       d.kind = m.kind;
       d.tex = m.texture;
-      d.albedo[0] = m.albedo.x, d.albedo[1] = m.albedo.y, d.albedo[2] = m.albedo.z;
-      d.fuzz = m.fuzz;
       d.ior = m.refraction_index;
+      if (m.kind == RT_MAT_DIELECTRIC) { // no albedo/fuzz: the union holds the constants
+        d.inv_ior = 1.0 / d.ior;
+        for (int f = 0; f < 2; ++f) {
+          const double ri = f == 0 ? d.inv_ior : d.ior;
+          double r0 = (1 - ri) / (1 + ri);
+          d.r0[f] = r0 * r0;
+        }
+      } else {
+        d.albedo[0] = m.albedo.x, d.albedo[1] = m.albedo.y, d.albedo[2] = m.albedo.z;
+        d.fuzz = m.fuzz;
+      }
       H.mats.push_back(d);
     }
     for (int i = 0; i < D->n_textures; ++i) {

@@ -128,3 +128,9 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
 extern "C" void emu_sincos_2pi(const double *u, int n, double *s, double *c) {
   for (int k = 0; k < n; ++k) rtp::sincos_2pi(u[k], s[k], c[k]);
 }
+
+// div_mk (Markstein quotient from a shared reciprocal) over n operand pairs
+// (its bit-exactness test, tests/test_emulator.py)
+extern "C" void emu_div_mk(const double *x, const double *b, int n, double *q) {
+  for (int k = 0; k < n; ++k) q[k] = rtp::div_mk(x[k], b[k], 1.0 / b[k]);
+}

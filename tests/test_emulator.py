@@ -65,3 +65,32 @@ def test_sincos_2pi_accuracy(emu):
     assert float(np.abs(c - np.cos(ang)).max()) < 3e-16
     assert np.all(np.abs(s) <= 1) and np.all(np.abs(c) <= 1)
     assert s[0] == 0.0 and c[0] == 1.0
+
+
+def test_div_mk_equals_division(emu):
+    """div_mk (rt_path.h: x * RN(1/b) plus one FMA correction, used for the sphere
+    roots and ct/pi) returns the IEEE division's double, bit for bit, on random
+    operands over the kernel's range, divisors with all-ones / all-zeros
+    significands, pi, and the ray-tracing magnitudes (|d|^2 ~ 1, roots ~ 1e-3..1e3)."""
+    rng = np.random.default_rng(11)
+    n = 400000
+
+    def rand_f64(lo_exp, hi_exp, m):
+        sig = rng.uniform(1.0, 2.0, size=m)
+        return sig * np.exp2(rng.integers(lo_exp, hi_exp, size=m).astype(np.float64))
+
+    x = rand_f64(-900, 900, n) * rng.choice([-1.0, 1.0], size=n)
+    b = rand_f64(-90, 90, n)
+    ones = np.nextafter(np.exp2(rng.integers(-60, 60, size=20000).astype(np.float64) + 1), 0)  # 1.111...1 x 2^e
+    pows = np.exp2(rng.integers(-60, 60, size=20000).astype(np.float64))
+    xb = rand_f64(-30, 30, 40000 + 20000) * rng.choice([-1.0, 1.0], size=60000)
+    bb = np.concatenate([ones, pows, np.full(20000, np.pi)])
+    x = np.concatenate([x, xb, rng.uniform(-1, 1, 100000)])
+    b = np.concatenate([b, bb, np.full(100000, np.pi)])
+    q = np.zeros_like(x)
+    P = C.POINTER(C.c_double)
+    emu.emu_div_mk.argtypes = [P, P, C.c_int, P]
+    emu.emu_div_mk(x.ctypes.data_as(P), b.ctypes.data_as(P), len(x), q.ctypes.data_as(P))
+    want = x / b
+    bad = q.view(np.uint64) != want.view(np.uint64)
+    assert not bad.any(), (x[bad][:4], b[bad][:4], q[bad][:4], want[bad][:4])
