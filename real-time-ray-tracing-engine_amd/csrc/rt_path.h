@@ -53,8 +53,34 @@ RT_HD RT_FI double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 RT_HD RT_FI V3 cross(V3 a, V3 b) {
   return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// Correctly rounded fp64 sqrt for x == 0 or x >= 2^-767 (and +inf, NaN, x < 0):
+// the compiler's own lowering (v_rsq_f64, Goldschmidt step, two Newton
+// corrections, zero/+inf class fixup) without its input scaling by 2^256 and
+// output scaling by 2^-128, which only matter below 2^-767 — 5 of 18
+// instructions.  Used where the input is a unit-range quantity known to be 0 or
+// far above 2^-767 (u = k 2^-32, 1 - u, 1 - x^2 of a double |x| <= 1, a squared
+// length compared against 1e-16); the root of a discriminant keeps sqrt().
+#ifndef RT_SQRT_N
+#define RT_SQRT_N 1
+#endif
+RT_HD RT_FI double sqrt_n(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && RT_SQRT_N
+  double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return __builtin_isfpclass(x, 0x260) ? x : g; // +-0, +inf: x itself
+#else
+  return sqrt(x);
+#endif
+}
 RT_HD RT_FI V3 unitv(V3 a) { // Vec3::normalize (Vec3.hpp:150-158)
-  double l = sqrt(len2(a));
+  double l = sqrt_n(len2(a)); // l <= 1e-8 (incl. every input below 2^-767) -> (1, 0, 0)
   if (l > 1e-8) {
     double s = 1.0 / l;
     return v3(a.x * s, a.y * s, a.z * s);
@@ -890,7 +916,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     if (STATS) cnt.wshade += wave_once();
     V3 refl = r.d - (2 * dot(r.d, h.n)) * h.n;
     double z = 1.0 - 2.0 * d0;
-    double rr = sqrt(fmax(0.0, 1.0 - z * z));
+    double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
     double sp, cp;
     sincos_2pi(d1, sp, cp);
     V3 uv = v3(rr * cp, rr * sp, z);
@@ -904,7 +930,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     double ri = h.front ? M.inv_ior : M.ior; // 1/ior formed on the host
     V3 ud = unitv(r.d);
     double ct = fmin(dot(-ud, h.n), 1.0);
-    double st = sqrt(1.0 - ct * ct);
+    double st = sqrt_n(1.0 - ct * ct);
     bool reflect_it = ri * st > 1.0;
     if (!reflect_it) {
       const double r0 = h.front ? M.r0[0] : M.r0[1]; // ((1 - ri) / (1 + ri))^2, host-formed
@@ -918,7 +944,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
       dir = ud - (2 * dot(ud, h.n)) * h.n;
     } else {
       V3 perp = ri * (ud + ct * h.n);
-      V3 par = (-sqrt(fabs(1.0 - len2(perp)))) * h.n;
+      V3 par = (-sqrt_n(fabs(1.0 - len2(perp)))) * h.n;
       dir = perp + par;
     }
     ps.ray = Ray{h.p, dir, r.tm};
@@ -949,12 +975,12 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
       double sp, cp;
       sincos_2pi(d0, sp, cp);
-      double sr = sqrt(d1);
-      V3 lc = v3(cp * sr, sp * sr, sqrt(1 - d1));
+      double sr = sqrt_n(d1);
+      V3 lc = v3(cp * sr, sp * sr, sqrt_n(1 - d1));
       gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
     } else {
       double z = 1.0 - 2.0 * d0;
-      double rr = sqrt(fmax(0.0, 1.0 - z * z));
+      double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
       double sp, cp;
       sincos_2pi(d1, sp, cp);
       gd = v3(rr * cp, rr * sp, z);
@@ -1005,7 +1031,7 @@ RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k
     double dk[4]; // slot 1: defocus disk (r^2, angle)
     u01x4<KB>(key, kCamTag, 1, dk);
     const double a = dk[0], b = dk[1];
-    double rr = sqrt(a);
+    double rr = sqrt_n(a);
     double s, c;
     sincos_2pi(b, s, c);
     double dx = rr * c, dy = rr * s;
