@@ -3,6 +3,7 @@
 // for bit (tests/test_gpu_arith.py):
 //   sqrt_n(x)           vs sqrt(x)      (the compiler's correctly rounded lowering)
 //   div_mk(x, b, 1/b)   vs x / b
+//   rcp_n(x)            vs 1.0 / x      (returned in the div_mk slot when b == 0)
 // Nothing on the product path links this.
 #include <hip/hip_runtime.h>
 
@@ -16,8 +17,13 @@ __global__ void arith_kernel(const double *x, const double *b, int n, double *sq
   const double xv = x[k], bv = b[k];
   sq_n[k] = rtp::sqrt_n(xv);
   sq[k] = sqrt(xv);
-  dq[k] = rtp::div_mk(xv, bv, 1.0 / bv);
-  dv[k] = xv / bv;
+  if (bv == 0.0) { // reciprocal mode
+    dq[k] = rtp::rcp_n(xv);
+    dv[k] = 1.0 / xv;
+  } else {
+    dq[k] = rtp::div_mk(xv, bv, 1.0 / bv);
+    dv[k] = xv / bv;
+  }
 }
 } // namespace
 

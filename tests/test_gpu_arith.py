@@ -5,7 +5,9 @@ on the GPU, against the full IEEE operations on the same device, bit for bit:
   sub-2^-767 input scaling — on every input range the kernel feeds it
   (u = k 2^-32, 1 - u, 1 - x^2, squared lengths, 0, +inf, negatives, NaN);
 * div_mk(x, b, 1/b) — the Markstein quotient from a shared reciprocal — on
-  random operands, divisors with all-ones / power-of-two significands, and pi.
+  random operands, divisors with all-ones / power-of-two significands, and pi;
+* rcp_n(x) — the division lowering for 1/x without scaling and fixup — on
+  [2^-600, 2^600], all-ones significands, the unit range, and +inf.
 
 tests/native/build/libdevcheck.so is test-only (tests/native/Makefile).
 """
@@ -74,3 +76,15 @@ def test_div_mk_equals_division_on_device(dev):
     _, _, dq, dv = run(dev, x, b)
     ok = same_bits(dq, dv)
     assert ok.all(), (x[~ok][:4], b[~ok][:4], dq[~ok][:4], dv[~ok][:4])
+
+
+def test_rcp_n_equals_reciprocal_on_device(dev):
+    rng = np.random.default_rng(6)
+    n = 1_000_000
+    x = rng.uniform(1.0, 2.0, n) * np.exp2(rng.integers(-600, 601, n).astype(np.float64))
+    ones = np.nextafter(np.exp2(rng.integers(-600, 600, 100_000).astype(np.float64) + 1), 0)
+    unit = rng.uniform(1e-8, 4.0, 300_000)
+    x = np.concatenate([x, ones, unit, [np.inf, 1.0, 1e-8, 2.0**512, 1.3407807929942596e154]])
+    _, _, dq, dv = run(dev, x, np.zeros_like(x))
+    ok = same_bits(dq, dv)
+    assert ok.all(), (x[~ok][:4], dq[~ok][:4], dv[~ok][:4])
