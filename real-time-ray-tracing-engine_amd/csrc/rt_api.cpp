@@ -100,6 +100,7 @@ int to_device_camera(const rt_frame *f, DCamera &c) {
   c.W = f->image_width;
   c.H = f->image_height;
   c.sqrt_spp = f->sqrt_spp;
+  c.rs = 1.0 / c.sqrt_spp;
   c.max_depth = f->max_depth;
   return RT_OK;
 }

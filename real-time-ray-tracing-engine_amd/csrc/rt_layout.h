@@ -107,7 +107,7 @@ struct DTex {        // 48 B
   int32_t kind, even, odd, perlin;
   double scale;
   double color[3];
-  double pad;
+  double inv_scale; // checker: 1.0 / scale formed on the host (CheckerTexture.cpp:19)
 };
 
 struct DPerlin {
@@ -160,6 +160,7 @@ struct DCamera {     // the rt_frame values the kernel needs
   double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
   double defocus_angle;
   double scale;
+  double rs; // 1.0 / sqrt_spp, formed on the host (Camera::initialize's recip_sqrt_spp)
   int32_t W, H, sqrt_spp, max_depth;
 };
 

@@ -250,7 +250,7 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
     const DTex &T = S.texs[t];
     if (T.kind == RT_TEX_SOLID) return ld3(T.color);
     if (T.kind == RT_TEX_CHECKER) { // CheckerTexture.cpp:41-55
-      double inv = 1.0 / T.scale;
+      const double inv = T.inv_scale; // 1.0 / scale, host-formed
       int xi = (int)floor(inv * p.x), yi = (int)floor(inv * p.y), zi = (int)floor(inv * p.z);
       t = ((xi + yi + zi) % 2 == 0) ? T.even : T.odd;
       continue;
@@ -1040,7 +1040,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
 template <bool KB = false> // KB: philox10
 RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
-  double rs = 1.0 / C.sqrt_spp;
+  const double rs = C.rs; // 1.0 / sqrt_spp (host-formed)
   double jt[4]; // slot 0: jitter x, jitter y, time
   u01x4<KB>(key, kCamTag, 0, jt);
   const double ja = jt[0], jb = jt[1];

@@ -686,6 +686,7 @@ struct Compiler {
       d.odd = t.odd;
       d.perlin = t.perlin;
       d.scale = t.scale;
+      d.inv_scale = 1.0 / t.scale;
       d.color[0] = t.color.x, d.color[1] = t.color.y, d.color[2] = t.color.z;
       H.texs.push_back(d);
     }

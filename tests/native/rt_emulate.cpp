@@ -102,6 +102,7 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   C.W = f->image_width;
   C.H = f->image_height;
   C.sqrt_spp = f->sqrt_spp;
+  C.rs = 1.0 / C.sqrt_spp;
   C.max_depth = f->max_depth;
   int r0 = p->row_begin, r1 = p->row_end;
   if (r0 == 0 && r1 == 0) r1 = f->image_height;
