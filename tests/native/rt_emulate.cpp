@@ -135,3 +135,24 @@ extern "C" void emu_sincos_2pi(const double *u, int n, double *s, double *c) {
 extern "C" void emu_div_mk(const double *x, const double *b, int n, double *q) {
   for (int k = 0; k < n; ++k) q[k] = rtp::div_mk(x[k], b[k], 1.0 / b[k]);
 }
+
+// Conservativeness of the kernel's fp32 slab tests (tests/test_emulator.py):
+// for n rays (o, d: 3 doubles each) against n boxes (lo, hi: 3 floats each) and
+// windows [tmin, tmax] (floats), out[k] = 1 if the subtract-form test passes,
+// | 2 if the FMA-form test passes.
+extern "C" void emu_slab(const double *o, const double *d, const float *lo, const float *hi,
+                         const float *tmin, const float *tmax, int n, int *out) {
+  for (int k = 0; k < n; ++k) {
+    rtp::Ray r;
+    r.o = rtp::v3(o[3 * k], o[3 * k + 1], o[3 * k + 2]);
+    r.d = rtp::v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]);
+    r.tm = 0.0;
+    const rtp::RayF<false> qs = rtp::ray_f32<false>(r);
+    const rtp::RayF<true> qf = rtp::ray_f32<true>(r);
+    const float inf = __builtin_huge_valf();
+    int v = 0;
+    if (rtp::slab<false>(qs, lo + 3 * k, hi + 3 * k, tmin[k], tmax[k]) != inf) v |= 1;
+    if (rtp::slab<true>(qf, lo + 3 * k, hi + 3 * k, tmin[k], tmax[k]) != inf) v |= 2;
+    out[k] = v;
+  }
+}

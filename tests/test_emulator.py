@@ -94,3 +94,72 @@ def test_div_mk_equals_division(emu):
     want = x / b
     bad = q.view(np.uint64) != want.view(np.uint64)
     assert not bad.any(), (x[bad][:4], b[bad][:4], q[bad][:4], want[bad][:4])
+
+
+def test_slab_tests_are_conservative(emu):
+    """Both fp32 slab forms of rt_path.h (subtract form: flat instances' medium cull;
+    FMA form with absolute slack: BVH instances) pass every box that the exact
+    slab test (long double) hits within the window — on random, grazing
+    (origin on a face plane), axis-parallel, tiny-component and large-coordinate
+    rays.  Visiting more boxes is allowed; dropping one is not."""
+    rng = np.random.default_rng(21)
+    n = 300_000
+    scale = np.exp2(rng.uniform(-8, 20, n))[:, None]
+    c = rng.uniform(-1, 1, (n, 3)) * scale
+    ext = rng.uniform(1e-4, 1, (n, 3)) * scale * np.exp2(rng.uniform(-10, 0, n))[:, None]
+    lo = (c - ext).astype(np.float32)
+    hi = (c + ext).astype(np.float32)
+    o = rng.uniform(-3, 3, (n, 3)) * scale
+    kind = rng.integers(0, 7, n)
+    onface = kind == 1                                    # origin exactly on a face plane
+    ax = rng.integers(0, 3, n)
+    o[onface, ax[onface]] = lo[onface, ax[onface]]
+    target = lo + rng.uniform(0, 1, (n, 3)) * (hi.astype(np.float64) - lo)
+    d = (target - o) * rng.uniform(0.5, 2, n)[:, None]
+    par = kind == 2                                       # axis-parallel rays
+    d[par, ax[par]] = 0.0
+    tiny = kind == 3                                      # tiny components
+    d[tiny, ax[tiny]] *= 1e-20
+    big = kind == 4                                       # far origin, small box
+    o[big] = o[big] * 1e3
+    d[big] = target[big] - o[big]
+    graze = kind >= 5                                     # through a corner region, far origin:
+    corner = np.where(rng.uniform(size=(n, 3)) < 0.5, lo, hi).astype(np.float64)  # tiny exact
+    inward = np.where(corner == lo, 1.0, -1.0) * (hi.astype(np.float64) - lo)      # intervals, large
+    target_g = corner + inward * np.exp2(rng.uniform(-30, -8, n))[:, None]         # |o / d|
+    o[graze] = c[graze] + rng.uniform(-1, 1, (int(graze.sum()), 3)) * scale[graze] * 1e3
+    d[graze] = target_g[graze] - o[graze]
+    tmin = np.full(n, np.float32(0.001) - np.float32(1e-10), dtype=np.float32)
+    tmax = np.where(rng.uniform(size=n) < 0.5, np.inf, rng.uniform(0.1, 3, n)).astype(np.float32)
+
+    L = np.longdouble
+    lo_l, hi_l, o_l, d_l = lo.astype(L), hi.astype(L), o.astype(L), d.astype(L)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t1 = (lo_l - o_l) / d_l
+        t2 = (hi_l - o_l) / d_l
+    near = np.minimum(t1, t2)
+    far = np.maximum(t1, t2)
+    zero = d_l == 0
+    inside = (lo_l <= o_l) & (o_l <= hi_l)
+    near = np.where(zero, np.where(inside, -np.inf, np.inf), near)
+    far = np.where(zero, np.where(inside, np.inf, -np.inf), far)
+    tl = np.maximum(near.max(axis=1), tmin.astype(L))
+    th = np.minimum(far.min(axis=1), tmax.astype(L))
+    margin = L(2.0) ** -40 * np.maximum(np.abs(tl), np.abs(th))
+    hit = th - tl > margin
+
+    out = np.zeros(n, dtype=np.int32)
+    PD, PF = C.POINTER(C.c_double), C.POINTER(C.c_float)
+    emu.emu_slab.argtypes = [PD, PD, PF, PF, PF, PF, C.c_int, C.POINTER(C.c_int)]
+    o_c, d_c = np.ascontiguousarray(o), np.ascontiguousarray(d)
+    lo_c, hi_c = np.ascontiguousarray(lo), np.ascontiguousarray(hi)
+    emu.emu_slab(o_c.ctypes.data_as(PD), d_c.ctypes.data_as(PD), lo_c.ctypes.data_as(PF),
+                 hi_c.ctypes.data_as(PF), tmin.ctypes.data_as(PF), tmax.ctypes.data_as(PF), n,
+                 out.ctypes.data_as(C.POINTER(C.c_int)))
+    assert hit.sum() > n // 4                            # the cases do exercise hits
+    for bit, form in ((1, "subtract"), (2, "fma")):
+        dropped = hit & ((out & bit) == 0)
+        assert not dropped.any(), "%s form dropped %d boxes, e.g. o=%s d=%s lo=%s hi=%s" % (
+            form, dropped.sum(), o[dropped][0], d[dropped][0], lo[dropped][0], hi[dropped][0])
+    # and they are not vacuous: most exact misses are culled
+    assert ((out & 2) == 0)[~hit].mean() > 0.5
