@@ -134,6 +134,14 @@ struct Key {
 // cost a v_readlane (plus hazard nops) per use.  Measured per instance: the
 // plain flat instance gains (C2 +3 %); the rich instances lose badly (C4 -25 %,
 // more SGPR pressure there), so only the former sets it.
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32
+RT_HD RT_FI uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 template <bool KB = false>
 RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                          uint32_t k0, uint32_t k1, uint32_t out[4]) {
@@ -149,7 +157,7 @@ RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
     // one 32x32->64 product per multiplier (v_mad_u64_u32), not a separate
     // mul_hi + mul_lo pair: half the quarter-rate integer multiplies
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0), n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c0 = n0;
     c1 = (uint32_t)p1;
     c2 = n2;
