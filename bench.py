@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--share-device", action="store_true")
     ap.add_argument("--shard", default="tiles", choices=["tiles", "strata"],
                     help="N>1: tiles round-robin + gather (default) or strata + reduce")
+    ap.add_argument("--n1-layout", default="frame", choices=["frame", "tiles"],
+                    help="N=1: render straight into the frame (default) or in 8x8 tile "
+                         "work units + chunk sum + tile->frame reorder, as the N>1 path")
     ap.add_argument("--check", action="store_true",
                     help="rank 0 compares the reduced frame with a 1-device render")
     args = ap.parse_args()
@@ -147,7 +150,7 @@ def main():
     n_strata = sq * sq
     s0 = rank * n_strata // ws
     s1 = (rank + 1) * n_strata // ws
-    tiles_mode = ws > 1 and args.shard == "tiles"
+    tiles_mode = (ws > 1 and args.shard == "tiles") or (ws == 1 and args.n1_layout == "tiles")
 
     from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks
     R = Renderer(scene, device=local)
@@ -186,7 +189,8 @@ def main():
             work.wait()
         if rank == 0:
             if tiles_mode:
-                final["frame"] = shard.frame_sums(gath[b])  # reorder the gathered tiles
+                # reorder the gathered tiles (N=1: this rank's own tile sums)
+                final["frame"] = shard.frame_sums(gath[b] if ws > 1 else tsum[b].unsqueeze(0))
             else:
                 final["frame"] = bufs[b]
             final["step"] = k
@@ -306,7 +310,8 @@ def main():
         "data": "synthetic: JSON scene %s, seeded Philox sample stream" % name,
         "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
                    "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
-                   "parallelism": ("1 GPU" if ws == 1 else
+                   "parallelism": (("1 GPU, tile work units x%d chunks" % shard.chunks
+                                    if tiles_mode else "1 GPU") if ws == 1 else
                                    "tile-shard x%d (tile t on rank t %% %d, %d stratum chunks) + %s gather" % (
                                        ws, ws, shard.chunks,
                                        "RCCL" if args.backend == "nccl" else "gloo")
