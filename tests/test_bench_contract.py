@@ -1,4 +1,5 @@
-"""bench.py's output contract, run end to end on one GPU at the C1 size.
+"""bench.py's output contract, run end to end on one GPU at the C1 size (N=1 and
+a 2-rank rehearsal of the N>1 path).
 
 One bench process per case (sequential, one GPU user at a time): the JSON line
 carries the driver's keys, the roofline / cpu-baseline-free fields, and its
@@ -37,4 +38,31 @@ def test_bench_line(layout):
     assert rf["kernel_ms"] > 0 and rf["achieved"] > 0 and rf["frac"] == pytest.approx(
         rf["achieved"] / rf["peak"], rel=1e-3)
     assert d["config"]["width"] == 400 and d["config"]["spp"] == 9
+    assert d["check"]["ok"], d["check"]
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shard", ["tiles", "strata"])
+def test_bench_two_ranks_one_gpu(shard):
+    """The N>1 bench path (tile gather / stratum reduce, double-buffered) with 2
+    ranks sharing cuda:0 and gloo standing in for RCCL; rank 0's frame must match
+    a single-device render (--check)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C1", "--steps", "2",
+           "--warmup", "1", "--backend", "gloo", "--share-device", "--check", "--shard", shard]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["check"]["ok"], d["check"]
