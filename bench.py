@@ -11,11 +11,15 @@ xGMI brings the compact tile sums to rank 0; --shard strata splits the strata
 instead and combines full-frame sums with an RCCL reduce(sum).  Strong scaling:
 the frame is fixed, N varies.
 
-Output: ONE JSON line on rank 0 (driver contract) with a roofline object (the
-render kernel's algorithmic bytes / HIP-event duration vs HBM peak), a "valu"
-object (the kernel's real ceiling: fp64 FLOP/s and VALU issue occupancy from the
-committed PMC pass, profiles/pmc_<config>.json) and a CPU baseline (the
-reference's own code on the host cores, bounded sample).
+Output: ONE JSON line on rank 0 (driver contract) with
+  * a roofline object for the render kernel: bound "valu" (the kernel issues
+    vector instructions most cycles; the scene is cache/LDS-resident), frac =
+    VALU-busy from rocprofv3 PMC passes that bench.py runs on this build and
+    workload before the timed run; physical HBM bytes per launch (traffic) and
+    GB/s, fp64 TFLOP/s, and SURVEY §8(d)'s algorithmic bytes as the
+    cache-served figure beside it;
+  * a CPU baseline: the reference's own StaticCamera::render -p (ThreadPool of
+    hardware_concurrency() workers) on the host cores, bounded sample.
 """
 import argparse
 import json
@@ -66,31 +70,169 @@ def algorithmic_bytes(st, info, n_pixels):
     return b
 
 
-def cpu_baseline(scene, cam_full, threads):
-    """The reference's own C++ path (oracle/_ref, built from /root/reference/src)
-    with its -p decomposition over `threads` host threads, on a bounded sample:
-    the full frame at 5x5 strata (same scene, depth, resolution; ~15 s)."""
+PMC_PASSES = {  # one rocprofv3 --pmc run each (TCC slots: FETCH_SIZE 3, WRITE_SIZE 2 of 4)
+    "valu": ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+             "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64", "GRBM_GUI_ACTIVE"],
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+}
+
+
+def pmc_counters(path_glob_root, kernel_tag="render_tiles<false"):
+    """Per-launch averages of every counter in the rocprofv3 counter-collection
+    CSVs under `path_glob_root`, over the render kernel's plain instance."""
+    import csv
+    import glob
+    sums, counts = {}, {}
+    for f in glob.glob(os.path.join(path_glob_root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel_tag not in r.get("Kernel_Name", ""):
+                continue
+            k = r["Counter_Name"]
+            sums[k] = sums.get(k, 0.0) + float(r["Counter_Value"])
+            counts[k] = counts.get(k, 0) + 1
+    return {k: sums[k] / counts[k] for k in sums}, max(counts.values()) if counts else 0
+
+
+def pmc_live(args):
+    """rocprofv3 PMC passes over THIS build and workload, run by bench.py itself
+    before it touches the GPU (each pass: a child `bench.py --pmc off` of the
+    same config, 1 warmup + 2 steps; counters averaged over the plain render
+    kernel's launches).  Returns the summary dict or None (no rocprofv3 / a pass
+    failed: the caller falls back to the committed profiles/pmc_<config>.json)."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    tmp = tempfile.mkdtemp(prefix="rtx_pmc_")
+    child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2",
+             "--warmup", "1", "--no-cpu-baseline", "--pmc", "off"]
+    if args.width:
+        child += ["--width", str(args.width)]
+    if args.spp:
+        child += ["--spp", str(args.spp)]
+    res = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for name, ctrs in PMC_PASSES.items():
+        d = os.path.join(tmp, name)
+        cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc"] + ctrs + [
+            "--output-format", "csv", "-d", d, "-o", name, "--"] + child
+        print("bench: PMC pass %s (%s)" % (name, " ".join(ctrs)), file=sys.stderr, flush=True)
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
+                               timeout=260)
+        except subprocess.TimeoutExpired:
+            return None
+        if r.returncode != 0:
+            print("bench: PMC pass %s failed (rc %d): %s" % (name, r.returncode,
+                                                               r.stderr.decode()[-400:]),
+                  file=sys.stderr)
+            return None
+        c, n = pmc_counters(d)
+        if not n or any(k not in c for k in ctrs):
+            return None
+        res.update(c)
+        res["launches_" + name] = n
+    f64 = sum(res[k] for k in PMC_PASSES["valu"][2:6])
+    return {
+        "source": "live: rocprofv3 --pmc passes run by bench.py on this build and workload",
+        "hbm_read_bytes_per_launch": int(2 * res["FETCH_SIZE"] * 1024),
+        "hbm_write_bytes_per_launch": int(res["WRITE_SIZE"] * 1024),
+        "hbm_bytes_per_launch": int(2 * res["FETCH_SIZE"] * 1024 + res["WRITE_SIZE"] * 1024),
+        "valu_insts_per_launch": int(res["SQ_INSTS_VALU"]),
+        "f64_insts_per_launch": int(f64),
+        "f64_flops_per_launch": int(64 * (f64 - res["SQ_INSTS_VALU_FMA_F64"])
+                                    + 128 * res["SQ_INSTS_VALU_FMA_F64"]),
+        "valu_busy": round(4 * res["SQ_ACTIVE_INST_VALU"] / (res["GRBM_GUI_ACTIVE"] / 8 * 1024), 4),
+        "launches": [res["launches_" + k] for k in PMC_PASSES],
+    }
+
+
+def host_cpu_info():
+    """Host cores as the reference sees them (std::thread::hardware_concurrency()
+    == os.cpu_count()), the cores this process may run on, the cgroup CPU quota
+    and the CPU model."""
+    info = {"hardware_concurrency": os.cpu_count() or 1}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(scene, cam_full):
+    """The reference's OWN multithreaded CPU path: StaticCamera::render with -p
+    (use_parallelism), i.e. render_cpu's ThreadPool of
+    std::thread::hardware_concurrency() workers, one task per pixel, a barrier per
+    row, and its PPM writer (StaticCamera.cpp:32-100, ThreadPool.hpp:6-174),
+    compiled from /root/reference/src into oracle/_ref.
+
+    Bounded sample: the same scene and depth at 960x540 (the reference pool's
+    1024-slot Chase-Lev deque overflows on rows wider than 1023 pixels and
+    corrupts the heap -- measured: `malloc(): unaligned fastbin chunk detected`
+    at 1920 wide, WorkStealingDeque.hpp:29-43 vs :72-85 -- so the sample keeps
+    rows short), with the stratum count chosen from a 1-spp calibration run so
+    the timed run is ~15 s of CPU work."""
+    import ctypes as C
+    import tempfile
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    from rtx.scene import camera_desc  # noqa: F401
-    spp = 25
-    cam = scene.camera_desc(image_width=cam_full.image_width, samples_per_pixel=spp,
-                            max_depth=cam_full.max_depth)
-    if O.ref_available():
-        t = time.time()
-        n, _ = O.ref_trace_parallel(scene, cam, threads)
-        dt = time.time() - t
-        kind = "reference"
-    else:  # reference build absent: the oracle restatement, same decomposition
-        t = time.time()
-        O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=threads)
-        dt = time.time() - t
-        n = cam.image_width * max(1, int(cam.image_width / cam.aspect_ratio)) * spp
-        kind = "port"
-    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": kind,
-            "sample": "%dx%d @ %d spp, depth %d, %s, %.1f s" % (
-                cam.image_width, max(1, int(cam.image_width / cam.aspect_ratio)), spp,
-                cam.max_depth, scene_name_of(scene), dt)}
+    host = host_cpu_info()
+    width = 960
+    h = max(1, int(width / cam_full.aspect_ratio))
+
+    def run(spp):
+        cam = scene.camera_desc(image_width=width, samples_per_pixel=spp,
+                                max_depth=cam_full.max_depth)
+        d = scene.desc()
+        cwd = os.getcwd()
+        tmp = tempfile.mkdtemp(prefix="rtx_cpu_")
+        err = os.dup(2)
+        try:
+            os.chdir(tmp)  # the reference writes output/<file> under the cwd
+            with open(os.path.join(tmp, "clog.txt"), "w") as f:
+                os.dup2(f.fileno(), 2)  # its "Scanlines remaining" progress (std::clog)
+                t = time.perf_counter()
+                if O.ref_available():
+                    O.ref().ref_render_static(C.byref(d), C.byref(cam), 1, int(scene.use_bvh), 1,
+                                              b"cpu_baseline.ppm")
+                else:  # reference build absent: the oracle restatement, same decomposition
+                    O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=host["hardware_concurrency"])
+                dt = time.perf_counter() - t
+        finally:
+            os.dup2(err, 2)
+            os.close(err)
+            os.chdir(cwd)
+        return dt
+
+    t1 = run(1)
+    sq = max(1, min(16, int((15.0 / max(t1, 1e-3)) ** 0.5)))
+    spp = sq * sq
+    dt = run(spp) if spp > 1 else t1
+    n = width * h * spp
+    out = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s",
+           "cores": host["hardware_concurrency"],
+           "kind": "reference" if O.ref_available() else "port",
+           "sample": "StaticCamera::render -p (ThreadPool, hardware_concurrency() = %d workers), "
+                     "%s %dx%d @ %d spp, depth %d, %.1f s" % (
+                         host["hardware_concurrency"], scene_name_of(scene), width, h, spp,
+                         cam_full.max_depth, dt)}
+    out.update({k: v for k, v in host.items() if k != "hardware_concurrency"})
+    return out
 
 
 def scene_name_of(scene):
@@ -106,7 +248,6 @@ def main():
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
     # rehearsal of the N>1 path on one GPU: every rank on cuda:0, gloo all_reduce
     # instead of RCCL reduce (the driver's 8-GPU runs use the defaults)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
@@ -118,9 +259,16 @@ def main():
                          "work units + chunk sum + tile->frame reorder, as the N>1 path")
     ap.add_argument("--check", action="store_true",
                     help="rank 0 compares the reduced frame with a 1-device render")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "file", "off"],
+                    help="N=1 roofline counters: auto = rocprofv3 PMC passes of this build "
+                         "run before the timed run (fallback: the committed "
+                         "profiles/pmc_<config>.json), file = the committed file only")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
+    pmc = None
+    if ws == 1 and args.pmc == "auto":  # before this process initialises the GPU
+        pmc = pmc_live(args)
     import torch
     from rtx import abi
     from rtx.render import Renderer, camera_frame
@@ -271,29 +419,52 @@ def main():
     bytes_launch = algorithmic_bytes(st, info, px_launch)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc_path):
+    if pmc is None and ws == 1 and args.pmc != "off" and os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            pmc = {}
-    valu = None
-    if pmc.get("f64_flops_per_launch") and ws == 1:
-        # fp64 work per launch is a property of the workload (PMC pass on the same
-        # command); divided by this run's live HIP-event kernel time
-        tfs = pmc["f64_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
-        valu = {"bound": "valu_f64", "achieved": round(tfs, 3), "peak": F64_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": round(tfs / F64_PEAK_TFS, 4),
-                "valu_busy": pmc.get("valu_busy"),
-                "valu_insts_per_launch": pmc.get("valu_insts_per_launch"),
-                "f64_insts_per_launch": pmc.get("f64_insts_per_launch"),
-                "note": "f64 FLOP = 64 x (ADD+MUL+TRANS) + 128 x FMA wave-instructions "
-                        "(PMC, every lane counted); valu_busy = SQ_ACTIVE_INST_VALU x 4 / "
-                        "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the share of SIMD cycles "
-                        "issuing VALU — the bound this kernel runs against"}
+            pmc["source"] = "committed file profiles/pmc_%s.json (an earlier PMC run)" % args.config
+        except (OSError, ValueError):
+            pmc = None
+    kernel_s = avg_ms * 1e-3
+    # The binding roof is vector-ALU issue: the scene is
+    # L1/L2/LDS-resident, so HBM carries only the accumulator.  frac = VALU-busy,
+    # SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (GRBM_GUI_ACTIVE / 8 XCDs x 1024
+    # SIMDs), from the PMC passes; physical HBM traffic (FETCH_SIZE x 2 +
+    # WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) is reported beside it.
+    roof = {"bound": "valu", "unit": "fraction of SIMD cycles issuing VALU", "peak": 1.0,
+            "achieved": None, "frac": None, "traffic": None, "kernel_ms": round(avg_ms, 3)}
+    if pmc and pmc.get("valu_busy") is not None:
+        roof["achieved"] = roof["frac"] = pmc["valu_busy"]
+    if pmc and pmc.get("hbm_bytes_per_launch"):
+        tb = pmc["hbm_bytes_per_launch"]
+        roof["traffic"] = tb
+        roof["hbm"] = {"bytes_per_launch": tb, "read_bytes_per_launch": pmc.get("hbm_read_bytes_per_launch"),
+                       "write_bytes_per_launch": pmc.get("hbm_write_bytes_per_launch"),
+                       "achieved_gbs": round(tb / kernel_s / 1e9, 2), "peak_gbs": HBM_PEAK_GBS,
+                       "frac": round(tb / kernel_s / 1e9 / HBM_PEAK_GBS, 5)}
+    if pmc and pmc.get("f64_flops_per_launch"):
+        tfs = pmc["f64_flops_per_launch"] / kernel_s / 1e12
+        roof["f64"] = {"achieved_tflops": round(tfs, 3), "peak_tflops": F64_PEAK_TFS,
+                       "frac": round(tfs / F64_PEAK_TFS, 4),
+                       "valu_insts_per_launch": pmc.get("valu_insts_per_launch"),
+                       "f64_insts_per_launch": pmc.get("f64_insts_per_launch")}
+    if pmc:
+        roof["pmc_source"] = pmc.get("source")
+    # SURVEY §8(d)'s algorithmic bytes: what the traversal/shading reads from the
+    # scene tables per launch.  Served by LDS/L1/L2, not HBM -- a cache-side
+    # figure, never an HBM fraction.
+    roof["cache_served"] = {"bytes_per_launch": int(bytes_launch),
+                            "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
+                            "gbs": round(achieved, 1)}
+    roof["counters"] = st
+    roof["lane_utilisation"] = {
+        "traversal": round(st["node_visits"] / max(1, 64 * st["wave_node_iters"]), 4),
+        "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
+        "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
+        "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
+    roof["note"] = ("VALU-issue bound; N>1 lines carry no PMC data (traffic null)"
+                    if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")
 
     out = {
         "metric": BASELINE["metric"],
@@ -318,22 +489,12 @@ def main():
                                    if tiles_mode else
                                    "stratum-shard x%d + %s reduce(sum)" % (
                                        ws, "RCCL" if args.backend == "nccl" else "gloo"))},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": traffic, "kernel_ms": round(avg_ms, 3),
-                     "note": "achieved = SURVEY 8d algorithmic bytes / kernel time; the scene "
-                             "is L1/L2-resident, so it can exceed HBM peak; traffic = PMC "
-                             "FETCH_SIZE x2 + WRITE_SIZE per launch (the accumulator)",
-                     "bytes_per_launch": int(bytes_launch),
-                     "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
-                     "counters": st},
+        "roofline": roof,
     }
-    if valu is not None:
-        out["valu"] = valu
     if check is not None:
         out["check"] = check
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, cam, min(args.cpu_threads, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(scene, cam)
     if rank == 0:
         print(json.dumps(out), flush=True)
     R.close()

@@ -22,6 +22,11 @@
  *                        buffer on a caller stream (multi-GPU sample sharding / progressive
  *                        accumulation; the role of dynamic_render_tile_kernel's accumulation
  *                        buffer, CameraKernels.cu:206-236)
+ *   rt_multi_create / rt_multi_render / rt_multi_destroy
+ *                     <- StaticCamera::render_gpu's single-device batch loop
+ *                        (src/core/camera/StaticCamera.cpp:136-313) extended to N devices:
+ *                        one scene and one host thread per shard, 8x8 tiles dealt
+ *                        round-robin over the shards (SURVEY §8(b) "Threading")
  *   rt_last_error     <- replaces CUDA_CHECK's exit() and the converters' exceptions
  *                        (CudaMemoryUtility.cuh:9-15, HittableConverter.cuh:103-108): errors are
  *                        returned as negative codes, never thrown or exit()ed across the ABI.
@@ -306,6 +311,31 @@ int rt_last_kernel_ms(rt_scene *scene, double *ms);
    reference's write_color rule (ColorUtility.hpp:11-36). */
 int rt_to_bytes_device(const double *device_rgb, int64_t n_pixels, double scale,
                        uint8_t *device_bytes, void *hip_stream);
+
+/* ---- multi-device rendering (tile shards) -------------------------------- */
+typedef struct rt_multi rt_multi; /* opaque: one rt_scene per shard */
+
+/* One scene per shard, shard k on devices[k % n_devices] (n_shards may exceed
+   n_devices: virtual shards share a device).  The scenes are compiled and
+   uploaded by one host thread per shard. */
+int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
+                    int32_t n_shards, rt_multi **multi);
+
+/* rt_render over the shards: shard k renders the 8x8 tiles t = k (mod
+   n_shards) of the row range, all launched strata, in (tile, stratum chunk)
+   work units, on its own host thread; the host gathers the tile sums and adds
+   each pixel's chunk partials in chunk order.  params->tile_first/tile_stride/
+   layout must be 0/0-or-1/RT_LAYOUT_FRAME; params->strata_chunks 0 = the chunk
+   split rt_render's frame launch uses on shard 0's device, which makes the
+   output bit-identical to rt_render on one device.  Synchronous. */
+int rt_multi_render(rt_multi *multi, const rt_frame *frame, const rt_render_params *params,
+                    double *host_rgb);
+
+/* Device time (ms) of each shard's last render kernel (HIP events on its
+   launch stream); ms must hold n_shards doubles (0 for a shard with no tiles). */
+int rt_multi_shard_ms(rt_multi *multi, double *ms);
+
+int rt_multi_destroy(rt_multi *multi);
 
 #ifdef __cplusplus
 }

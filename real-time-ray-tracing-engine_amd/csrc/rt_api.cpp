@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_api.h"
@@ -553,6 +554,124 @@ int rt_to_bytes_device(const double *rgb, int64_t n, double scale, uint8_t *byte
   if (!rgb || !bytes || n < 0) return set_err(RT_ERR_INVALID, "invalid argument");
   hipError_t e = rtk_launch_to_bytes(rgb, n, scale, bytes, (hipStream_t)hip_stream);
   if (e != hipSuccess) return hip_err(e, "to_bytes launch");
+  return RT_OK;
+}
+
+// ---------------------------------------------------------------- multi-device
+// One rt_scene per shard, one host thread per shard (StaticCamera::render_gpu's
+// single-device loop, StaticCamera.cpp:136-313, spread over N devices).  Shard
+// k renders tiles k, k+N, k+2N, ... in the compact tile layout; the host adds
+// each pixel's chunk partials in chunk order -- the order chunk_sum_kernel
+// uses -- so with the frame launch's chunk split the frame is bit-identical to
+// rt_render on one device.
+struct rt_multi {
+  std::vector<rt_scene *> scenes; // one per shard
+  std::vector<std::vector<double>> parts;
+  std::vector<double> ms;
+};
+
+int rt_multi_destroy(rt_multi *m) {
+  if (!m) return RT_OK;
+  for (rt_scene *s : m->scenes) rt_scene_destroy(s);
+  delete m;
+  return RT_OK;
+}
+
+int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
+                    int32_t n_shards, rt_multi **out) {
+  if (!out || !desc || !devices) return set_err(RT_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (n_devices < 1 || n_shards < n_devices)
+    return set_err(RT_ERR_INVALID, "need n_devices >= 1 and n_shards >= n_devices");
+  rt_multi *m = new rt_multi();
+  m->scenes.assign(n_shards, nullptr);
+  m->parts.resize(n_shards);
+  m->ms.assign(n_shards, 0.0);
+  std::vector<int> rc(n_shards, RT_OK);
+  std::vector<std::string> err(n_shards);
+  std::vector<std::thread> th;
+  for (int k = 0; k < n_shards; ++k)
+    th.emplace_back([&, k]() {
+      rc[k] = rt_scene_create(desc, devices[k % n_devices], &m->scenes[k]);
+      if (rc[k] != RT_OK) err[k] = g_err; // thread-local message of this worker
+    });
+  for (auto &t : th) t.join();
+  for (int k = 0; k < n_shards; ++k)
+    if (rc[k] != RT_OK) {
+      rt_multi_destroy(m);
+      return set_err(rc[k], "shard " + std::to_string(k) + ": " + err[k]);
+    }
+  *out = m;
+  return RT_OK;
+}
+
+int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, double *host_rgb) {
+  if (!m || !host_rgb || !p) return set_err(RT_ERR_INVALID, "null argument");
+  if (p->tile_first != 0 || p->tile_stride > 1 || p->layout != RT_LAYOUT_FRAME)
+    return set_err(RT_ERR_INVALID, "rt_multi_render takes a whole-frame launch "
+                                   "(tile_first 0, tile_stride 0/1, RT_LAYOUT_FRAME)");
+  DCamera C;
+  DLaunch L;
+  int rc = to_device_camera(f, C);
+  if (rc) return rc;
+  rt_render_params full = *p;
+  full.strata_chunks = 0;
+  if ((rc = to_launch(f, &full, L))) return rc;
+  const int n = (int)m->scenes.size();
+  int chunks = p->strata_chunks;
+  if (chunks <= 0) chunks = frame_chunks(m->scenes[0], L);
+  chunks = std::max(1, std::min(chunks, std::max(1, L.sample_count)));
+  const int W = f->image_width, r0 = L.row_begin, r1 = L.row_end;
+  const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
+  std::vector<int> src(n, RT_OK);
+  std::vector<std::string> err(n);
+  std::vector<std::thread> th;
+  for (int k = 0; k < n; ++k) {
+    m->ms[k] = 0.0;
+    if (k >= n_tiles) continue; // more shards than tiles
+    th.emplace_back([&, k]() {
+      rt_render_params q = *p;
+      q.tile_first = k;
+      q.tile_stride = n;
+      q.layout = RT_LAYOUT_TILES;
+      q.strata_chunks = chunks;
+      q.output = RT_OUT_SUM;
+      q.accumulate = 0;
+      const int64_t local = (n_tiles - k + n - 1) / n;
+      m->parts[k].resize((size_t)local * chunks * 64 * 3);
+      src[k] = rt_render(m->scenes[k], f, &q, m->parts[k].data());
+      if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
+      if (src[k] != RT_OK) err[k] = g_err;
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int k = 0; k < n; ++k)
+    if (src[k] != RT_OK) return set_err(src[k], "shard " + std::to_string(k) + ": " + err[k]);
+  // gather: tile t = k + lt*n of shard k; pixel (x, y) of the tile at slot y*8+x
+  const bool scaled = p->output == RT_OUT_SCALED;
+  for (int k = 0; k < n && k < n_tiles; ++k) {
+    const double *part = m->parts[k].data();
+    for (int64_t t = k, lt = 0; t < n_tiles; t += n, ++lt) {
+      const int tx = (int)(t % L.tiles_x), ty = (int)(t / L.tiles_x);
+      for (int slot = 0; slot < 64; ++slot) {
+        const int i = tx * 8 + (slot & 7), j = r0 + ty * 8 + (slot >> 3);
+        if (i >= W || j >= r1) continue;
+        double *o = host_rgb + 3 * ((size_t)(j - r0) * W + i);
+        for (int ch = 0; ch < 3; ++ch) {
+          const double *pp = part + ((size_t)lt * chunks * 64 + slot) * 3 + ch;
+          double sum = pp[0];
+          for (int c = 1; c < chunks; ++c) sum += pp[(size_t)c * 64 * 3];
+          o[ch] = scaled ? C.scale * sum : sum;
+        }
+      }
+    }
+  }
+  return RT_OK;
+}
+
+int rt_multi_shard_ms(rt_multi *m, double *ms) {
+  if (!m || !ms) return set_err(RT_ERR_INVALID, "null argument");
+  for (size_t k = 0; k < m->ms.size(); ++k) ms[k] = m->ms[k];
   return RT_OK;
 }
 

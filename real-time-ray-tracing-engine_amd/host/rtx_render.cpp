@@ -7,7 +7,8 @@
 //
 //   rtx_render [--camera static] [--output image.ppm] [-p] [-b] [-g] [-d]
 //              [--width N] [--samples N] [--depth N]
-//              [--scene file.json] [--seed S] [--device D] [--dump-desc]
+//              [--scene file.json] [--seed S] [--device D] [--gpus N] [--shards K]
+//              [--dump-desc]
 //
 // Mapping of the reference flags onto this library:
 //   --camera static   the only mode; "dynamic" is the SDL window (out of scope,
@@ -24,7 +25,12 @@
 // Extensions: --scene (default scenes/cornell.json next to the library, the
 // reference's default populate_cornell_box_scene), --seed (the Philox key that
 // replaces curand_init(time(nullptr)+pixel)), --device, --dump-desc (print the
-// description as JSON and exit; used by tests/test_cli.py).
+// description as JSON and exit; used by tests/test_cli.py), and the multi-GPU
+// flags SURVEY §5 adds: --gpus N renders on devices device..device+N-1 through
+// rt_multi_* (one host thread and one scene per shard, 8x8 tiles dealt
+// round-robin, tile sums gathered on the host); --shards K (default N) splits
+// the frame into K tile shards, K > N putting several shards on one device.
+// The sharded frame is bit-identical to the one-device frame (rt_api.h).
 #include "rt_api.h"
 #include "scene_json.hpp"
 
@@ -48,6 +54,7 @@ struct Options {
   std::string scene;
   unsigned long long seed = 0;
   int device = 0;
+  int gpus = 1, shards = 0;
 };
 
 bool parse_int(const char *s, int &out) {
@@ -95,7 +102,8 @@ Options parse(int argc, char **argv) {
       o.gpu = true;
     } else if (a == "-d" || a == "--debug") {
       o.debug = true;
-    } else if (a == "--width" || a == "--samples" || a == "--depth" || a == "--device") {
+    } else if (a == "--width" || a == "--samples" || a == "--depth" || a == "--device" ||
+               a == "--gpus" || a == "--shards") {
       if (const char *v = need("a number")) {
         int x;
         if (!parse_int(v, x)) {
@@ -110,6 +118,10 @@ Options parse(int argc, char **argv) {
         } else if (a == "--depth") {
           o.depth = x;
           o.depth_set = true;
+        } else if (a == "--gpus") {
+          o.gpus = x;
+        } else if (a == "--shards") {
+          o.shards = x;
         } else {
           o.device = x;
         }
@@ -124,6 +136,10 @@ Options parse(int argc, char **argv) {
       o.any_errors = true;
       std::cerr << "Unknown option: " << a << std::endl;
     }
+  }
+  if (o.gpus < 1 || o.shards < 0 || (o.shards && o.shards < o.gpus)) {
+    o.any_errors = true;
+    std::cerr << "--gpus must be >= 1 and --shards >= --gpus\n";
   }
   if (!o.use_static && output_selected)
     std::cerr << "You can only set an output file if the static camera is selected, ignoring...\n";
@@ -148,6 +164,8 @@ void print_help() {
          "  --scene <file.json>        Scene file (default: scenes/cornell.json)\n"
          "  --seed <u64>               Sample-stream key (default: 0)\n"
          "  --device <int>             HIP device ordinal (default: 0)\n"
+         "  --gpus <int>               Devices to render on, from --device (default: 1)\n"
+         "  --shards <int>             Tile shards over those devices (default: --gpus)\n"
          "  --dump-desc                Print the flattened scene description and exit\n";
 }
 
@@ -320,7 +338,27 @@ int main(int argc, char **argv) {
   if (rt_camera_setup(&cam, &frame) != RT_OK) return fail_rt("camera");
   rt_scene_desc desc = S.desc();
   rt_scene *scene = nullptr;
-  if (rt_scene_create(&desc, opt.device, &scene) != RT_OK) return fail_rt("scene");
+  rt_multi *multi = nullptr;
+  const int shards = opt.shards ? opt.shards : opt.gpus;
+  if (shards > 1) {
+    int32_t ndev = 0;
+    if (rt_device_count(&ndev) != RT_OK) return fail_rt("device count");
+    if (opt.device < 0 || opt.device + opt.gpus > ndev) {
+      std::cerr << "[ERROR] --device " << opt.device << " --gpus " << opt.gpus << " needs "
+                << opt.device + opt.gpus << " devices, " << ndev << " present\n";
+      return 1;
+    }
+    std::vector<int32_t> devs;
+    for (int d = 0; d < opt.gpus; ++d) devs.push_back(opt.device + d);
+    if (rt_multi_create(&desc, devs.data(), opt.gpus, shards, &multi) != RT_OK)
+      return fail_rt("scene");
+  } else if (rt_scene_create(&desc, opt.device, &scene) != RT_OK) {
+    return fail_rt("scene");
+  }
+  auto release = [&]() {
+    if (scene) rt_scene_destroy(scene);
+    if (multi) rt_multi_destroy(multi);
+  };
 
   const int W = frame.image_width, H = frame.image_height;
   const int n_strata = frame.sqrt_spp * frame.sqrt_spp;
@@ -338,17 +376,21 @@ int main(int argc, char **argv) {
     p.sample_count = cnt;
     p.seed = opt.seed;
     p.output = RT_OUT_SUM;
-    if (rt_render(scene, &frame, &p, part.data()) != RT_OK) {
-      rt_scene_destroy(scene);
-      return fail_rt("render");
+    if ((multi ? rt_multi_render(multi, &frame, &p, part.data())
+               : rt_render(scene, &frame, &p, part.data())) != RT_OK) {
+      int rc = fail_rt("render");
+      release();
+      return rc;
     }
     for (size_t k = 0; k < sum.size(); ++k) sum[k] += part[k];
     std::clog << "\rStrata remaining: " << (n_strata - s - cnt) << ' ' << std::flush;
   }
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  rt_scene_destroy(scene);
+  release();
   std::clog << "\rDone. " << W << "x" << H << " @ " << n_strata << " spp, "
-            << (double)W * H * n_strata / secs / 1e6 << " Msamples/s\n";
+            << (double)W * H * n_strata / secs / 1e6 << " Msamples/s";
+  if (shards > 1) std::clog << " (" << shards << " tile shards on " << opt.gpus << " device(s))";
+  std::clog << "\n";
 
   mkdir("output", 0755);
   std::string path = "output/" + opt.output;

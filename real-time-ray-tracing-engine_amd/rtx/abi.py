@@ -117,4 +117,5 @@ EXPORTS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_camera_setup",
     "rt_scene_create", "rt_scene_info_get", "rt_scene_destroy", "rt_render",
     "rt_render_device", "rt_render_stats", "rt_last_kernel_ms", "rt_to_bytes_device",
+    "rt_multi_create", "rt_multi_render", "rt_multi_shard_ms", "rt_multi_destroy",
 )

@@ -7,8 +7,12 @@ Two decompositions of one frame over the ranks of the default process group:
   spread evenly; each rank renders ALL strata of its tiles into a compact tile
   buffer (RT_LAYOUT_TILES) and rank 0 gathers the buffers (1/world of the frame
   from each rank, over all of rank 0's xGMI links at once) and reorders them.
-  Every pixel is computed by exactly one GPU, so the frame is the one-GPU frame
-  bit for bit.
+  Every pixel is computed by exactly one GPU.  Its strata are split into the
+  rank's own chunk count (`auto_chunks`, sized for each rank's wave slots), not
+  the one-GPU frame launch's, so a pixel's chunk partials are added in a
+  different grouping: the frame equals the one-GPU frame up to fp64 summation
+  order (the 2-rank rehearsal measures 2.8e-14).  The C ABI's rt_multi_render
+  (strata_chunks 0) keeps the frame launch's split and is bit-identical.
 * stratum sharding (below): ranks split the strata and reduce(sum) full-frame
   accumulators — the SURVEY §8(e) recommendation; it moves ~2x the frame per
   rank through a ring and changes the fp64 summation order.

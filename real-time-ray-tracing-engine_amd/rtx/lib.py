@@ -49,6 +49,11 @@ def load():
     L.rt_render_stats.argtypes = [C.c_void_p, P(abi.Frame), P(abi.RenderParams), P(abi.PathStats)]
     L.rt_last_kernel_ms.argtypes = [C.c_void_p, P(C.c_double)]
     L.rt_to_bytes_device.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p, C.c_void_p]
+    L.rt_multi_create.argtypes = [P(abi.SceneDesc), P(C.c_int32), C.c_int32, C.c_int32,
+                                  P(C.c_void_p)]
+    L.rt_multi_render.argtypes = [C.c_void_p, P(abi.Frame), P(abi.RenderParams), P(C.c_double)]
+    L.rt_multi_shard_ms.argtypes = [C.c_void_p, P(C.c_double)]
+    L.rt_multi_destroy.argtypes = [C.c_void_p]
     for name in abi.EXPORTS:
         getattr(L, name).restype = C.c_char_p if name == "rt_last_error" else C.c_int
     if L.rt_abi_version() != 1:

@@ -121,6 +121,49 @@ class Renderer:
         return ms.value
 
 
+class MultiRenderer:
+    """rt_multi_*: one device scene per shard (shard k on devices[k % len]),
+    one host thread per shard, 8x8 tiles dealt round-robin; the multi-device
+    form of StaticCamera::render_gpu (StaticCamera.cpp:136-313)."""
+
+    def __init__(self, scene, devices=(0,), shards=None):
+        self.lib = load()
+        self._desc = scene.desc()
+        devs = (C.c_int32 * len(devices))(*devices)
+        self.n_shards = int(shards or len(devices))
+        h = C.c_void_p()
+        check(self.lib.rt_multi_create(C.byref(self._desc), devs, len(devices), self.n_shards,
+                                       C.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.rt_multi_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def render(self, frame, seed=0, rows=(0, 0), samples=(0, -1), output=abi.RT_OUT_SCALED,
+               chunks=0):
+        r0, r1 = rows
+        if r0 == 0 and r1 == 0:
+            r1 = frame.image_height
+        out = np.empty((max(0, r1 - r0), frame.image_width, 3), dtype=np.float64)
+        p = Renderer.params(seed, (r0, r1), samples, output, 0, (0, 1), abi.RT_LAYOUT_FRAME, chunks)
+        check(self.lib.rt_multi_render(self.handle, C.byref(frame), C.byref(p),
+                                       out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out
+
+    def shard_ms(self):
+        ms = (C.c_double * self.n_shards)()
+        check(self.lib.rt_multi_shard_ms(self.handle, ms))
+        return list(ms)
+
+
 def render_ppm(scene, path, device=0, seed=0, **cam_overrides):
     """StaticCamera::render on the HIP path: camera setup, render, PPM."""
     cam = scene.camera_desc(**cam_overrides)

@@ -18,10 +18,10 @@ KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline")
 
 
-def _bench(*extra):
+def _bench(*extra, timeout=110):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C1", "--steps", "2",
            "--warmup", "1", "--no-cpu-baseline", "--check", *extra]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -29,16 +29,29 @@ def _bench(*extra):
 @pytest.mark.gpu
 @pytest.mark.parametrize("layout", ["frame", "tiles"])
 def test_bench_line(layout):
-    d = _bench("--n1-layout", layout)
+    d = _bench("--n1-layout", layout, "--pmc", "file")
     for k in KEYS:
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["dtype"] == "f64"
     assert d["value"] > 0 and d["unit"] == "Msamples/s"
     rf = d["roofline"]
-    assert rf["kernel_ms"] > 0 and rf["achieved"] > 0 and rf["frac"] == pytest.approx(
-        rf["achieved"] / rf["peak"], rel=1e-3)
+    assert rf["bound"] == "valu" and rf["kernel_ms"] > 0
+    assert 0 < rf["achieved"] <= 1 and rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-3)
+    assert "committed" in rf["pmc_source"]
     assert d["config"]["width"] == 400 and d["config"]["spp"] == 9
     assert d["check"]["ok"], d["check"]
+
+
+@pytest.mark.gpu
+def test_bench_line_live_pmc():
+    """Default --pmc auto: bench.py runs the rocprofv3 PMC passes (VALU, FETCH_SIZE,
+    WRITE_SIZE) on this build before its timed run; the roofline is the VALU-busy
+    fraction (<= 1) and traffic the PMC HBM bytes."""
+    d = _bench(timeout=400)
+    rf = d["roofline"]
+    assert rf["pmc_source"].startswith("live"), rf.get("pmc_source")
+    assert 0 < rf["frac"] <= 1 and rf["traffic"] > 0
+    assert rf["hbm"]["frac"] < 1
 
 
 def _free_port():
