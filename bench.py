@@ -232,6 +232,27 @@ def cpu_baseline(scene, cam_full):
                          host["hardware_concurrency"], scene_name_of(scene), width, h, spp,
                          cam_full.max_depth, dt)}
     out.update({k: v for k, v in host.items() if k != "hardware_concurrency"})
+    # The box may cap this process below hardware_concurrency() (cgroup CPU
+    # quota): the reference's pool then oversubscribes the quota with spinning
+    # workers.  Beside the primary figure, the same -p loop on the reference's
+    # ThreadPool sized to the quota.
+    quota = host.get("cgroup_cpu_quota") or host.get("affinity_cpus")
+    if O.ref_available() and quota and int(quota) < host["hardware_concurrency"]:
+        nt = max(1, int(quota))
+        cam = scene.camera_desc(image_width=width, samples_per_pixel=1, max_depth=cam_full.max_depth)
+        t = time.perf_counter()
+        O.ref_trace_pool(scene, cam, nt)
+        t1 = time.perf_counter() - t
+        sq2 = max(1, min(16, int((10.0 / max(t1, 1e-3)) ** 0.5)))
+        cam = scene.camera_desc(image_width=width, samples_per_pixel=sq2 * sq2,
+                                max_depth=cam_full.max_depth)
+        t = time.perf_counter()
+        n2, _ = O.ref_trace_pool(scene, cam, nt)
+        dt2 = time.perf_counter() - t
+        out["quota_sized_pool"] = {
+            "value": round(n2 / dt2 / 1e6, 4), "unit": "Msamples/s", "cores": nt,
+            "sample": "render_cpu -p loop on the reference ThreadPool with %d workers, "
+                      "%dx%d @ %d spp, %.1f s" % (nt, width, h, sq2 * sq2, dt2)}
     return out
 
 

@@ -36,8 +36,10 @@
 #include "scene/textures/NoiseTexture.hpp"
 #include "scene/textures/SolidColorTexture.hpp"
 #include "utils/ColorUtility.hpp"
+#include "utils/concurrency/ThreadPool.hpp"
 #include "ref_binding.hpp"
 #include "utils/math/Utility.hpp"
+#include "utils/math/Vec3Utility.hpp"
 
 #include <atomic>
 #include <cstring>
@@ -204,6 +206,36 @@ struct GoldenCamera : public Camera {
         o[2] = sc.z();
       }
   }
+  // StaticCamera::render_cpu's -p loop (StaticCamera.cpp:59-100) on the
+  // reference's own ThreadPool (ThreadPool.hpp:6-174), sized by the caller
+  // instead of hardware_concurrency(); radiance kept instead of quantised.
+  long long trace_pool(HittableList &world, HittableList &lights, int threads, double *out) {
+    ThreadPool pool(threads);
+    std::vector<Color> row_colors(m_image_width);
+    const int sqrt_spp = static_cast<int>(std::sqrt(m_samples_per_pixel));
+    for (int j = 0; j < m_image_height; ++j) {
+      pool.start();
+      for (int i = 0; i < m_image_width; ++i) {
+        pool.submit_job([this, &world, &lights, i, j, sqrt_spp, &row_colors]() {
+          row_colors[i] = Color(0, 0, 0);
+          for (int s_j = 0; s_j < sqrt_spp; ++s_j)
+            for (int s_i = 0; s_i < sqrt_spp; ++s_i) {
+              Ray ray = get_ray(i, j, s_i, s_j);
+              row_colors[i] += ray_color(ray, m_max_depth, world, lights);
+            }
+        });
+      }
+      pool.finish();
+      for (int i = 0; i < m_image_width; ++i) {
+        Color sc = m_pixel_samples_scale * row_colors[i];
+        double *o = out + 3 * ((size_t)j * m_image_width + i);
+        o[0] = sc.x();
+        o[1] = sc.y();
+        o[2] = sc.z();
+      }
+    }
+    return (long long)m_image_width * m_image_height * sqrt_spp * sqrt_spp;
+  }
   long long trace_parallel(HittableList &world, HittableList &lights, int threads, double *out) {
     int sq = static_cast<int>(std::sqrt(m_samples_per_pixel));
     for (int j = 0; j < m_image_height; ++j) {
@@ -317,6 +349,24 @@ long long ref_trace_parallel(const rt_scene_desc *d, const rt_camera_desc *cam, 
   return c.trace_parallel(world, lights, threads, out);
 }
 
+/* CPU baseline, quota-sized: render_cpu's -p decomposition on the reference's
+   own ThreadPool with `threads` workers (the reference sizes it by
+   hardware_concurrency(), StaticCamera.cpp:60). */
+long long ref_trace_pool(const rt_scene_desc *d, const rt_camera_desc *cam, int use_bvh,
+                         int threads, double *out) {
+  Graph g;
+  g.load(d);
+  HittableList world, lights;
+  root_lists(g, d, world, lights);
+  GoldenCamera c(make_config(cam, use_bvh != 0, true));
+  c.setup();
+  if (use_bvh) {
+    if (!world.get_objects().empty()) world = HittableList(std::make_shared<BVHNode>(world));
+    if (!lights.get_objects().empty()) lights = HittableList(std::make_shared<BVHNode>(lights));
+  }
+  return c.trace_pool(world, lights, threads, out);
+}
+
 int ref_object_hit(const rt_scene_desc *d, int obj, const double ray[7], double tmin, double tmax,
                    double res[12]) {
   Graph g;
@@ -364,5 +414,45 @@ void ref_texture_value(const rt_scene_desc *d, int t, double u, double v, const 
 }
 
 unsigned char ref_to_byte(double x) { return to_byte(x); }
+
+/* Distribution KATs: n draws of the reference's own samplers from the seeded
+   main-thread engine -- kind 0 random_unit_vector (rejection loop,
+   Vec3Utility.hpp:53-64), 1 random_in_unit_disk (Vec3Utility.hpp:41-51), 2
+   random_cosine_direction (Vec3Utility.hpp:94-103).  out: n x 3. */
+int ref_sample_batch(int kind, uint32_t seed, int n, double *out) {
+  random_engine().seed(seed);
+  for (int k = 0; k < n; ++k) {
+    Vec3 v = kind == 0 ? random_unit_vector() : kind == 1 ? random_in_unit_disk()
+                                                          : random_cosine_direction();
+    out[3 * k] = v.x();
+    out[3 * k + 1] = v.y();
+    out[3 * k + 2] = v.z();
+  }
+  return kind >= 0 && kind <= 2 ? 0 : -1;
+}
+
+/* n light directions from `org`: the reference's lights.random(org) -- the
+   HittableList (HittableList.cpp:58-63) or, with use_bvh, HittableList(BVHNode)
+   (BVHNode.cpp:149-166) over Plane::random / Sphere::random (Plane.cpp:128-132,
+   Sphere.cpp:160-178) and the RotateY / Translate wrappers.  out: n x 3. */
+int ref_light_batch(const rt_scene_desc *d, int use_bvh, const double org[3], uint32_t seed, int n,
+                    double *out) {
+  if (d->lights < 0) return -1;
+  Graph g;
+  g.load(d);
+  HittableList world, lights;
+  root_lists(g, d, world, lights);
+  if (use_bvh && !lights.get_objects().empty())
+    lights = HittableList(std::make_shared<BVHNode>(lights));
+  random_engine().seed(seed);
+  Point3 o(org[0], org[1], org[2]);
+  for (int k = 0; k < n; ++k) {
+    Vec3 v = lights.random(o);
+    out[3 * k] = v.x();
+    out[3 * k + 1] = v.y();
+    out[3 * k + 2] = v.z();
+  }
+  return 0;
+}
 
 } // extern "C"

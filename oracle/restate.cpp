@@ -1339,4 +1339,48 @@ void oracle_texture_value(const rt_scene_desc *D, int t, double u, double v, con
   out[2] = c.z;
 }
 
+/* Distribution KATs (tests/test_distributions.py): n draws of the COUNTER-mode
+   samplers, draw k from the Philox block (seed; pixel k, sample 0, bounce 0,
+   slot) exactly as the integrator consumes it -- kind 0 ctr_unit_vector and 2
+   cosine_dir from the shading block's direction uniforms (d2, d3; slot 0,
+   ray_color), 1 ctr_in_unit_disk from the camera's defocus block (d0, d1;
+   CAM_TAG, slot 1, get_ray).  out: n x 3. */
+int oracle_ctr_sample_batch(int kind, uint64_t seed, int n, double *out) {
+  for (int k = 0; k < n; ++k) {
+    double d[4];
+    V v;
+    if (kind == 1) {
+      oracle_philox_u01x4(seed, (uint32_t)k, 0, CAM_TAG, 1, d);
+      v = ctr_in_unit_disk(d[0], d[1]);
+    } else {
+      oracle_philox_u01x4(seed, (uint32_t)k, 0, 0, SLOT_SHADE, d);
+      v = kind == 0 ? ctr_unit_vector(d[2], d[3]) : cosine_dir(d[2], d[3]);
+    }
+    out[3 * k] = v.x;
+    out[3 * k + 1] = v.y;
+    out[3 * k + 2] = v.z;
+  }
+  return kind >= 0 && kind <= 2 ? 0 : -1;
+}
+
+/* n COUNTER-mode light directions from `org` (ctr_light_random: leaf pick by
+   cumulative weight from d1, direction from d2, d3 of the shading block). */
+int oracle_ctr_light_batch(const rt_scene_desc *D, int use_bvh, const double org[3], uint64_t seed,
+                           int n, double *out) {
+  Scene S;
+  if (build_scene(S, D, use_bvh) != 0 || S.leaves.empty()) return -1;
+  Sampler s{MODE_COUNTER, nullptr, seed, 0, 0, 0};
+  Ctx C{&S, &s};
+  V o = mk(org[0], org[1], org[2]);
+  for (int k = 0; k < n; ++k) {
+    double d[4];
+    oracle_philox_u01x4(seed, (uint32_t)k, 0, 0, SLOT_SHADE, d);
+    V v = ctr_light_random(C, o, d[1], d[2], d[3]);
+    out[3 * k] = v.x;
+    out[3 * k + 1] = v.y;
+    out[3 * k + 2] = v.z;
+  }
+  return 0;
+}
+
 } // extern "C"

@@ -144,3 +144,58 @@ def ref_trace_parallel(scene, cam, threads, use_bvh=None):
     L.ref_trace_parallel.restype = C.c_longlong
     n = L.ref_trace_parallel(C.byref(d), C.byref(cam), int(bvh), int(threads), dptr(out))
     return n, out
+
+
+def ref_trace_pool(scene, cam, threads, use_bvh=None):
+    """Reference code, render_cpu's -p loop on the reference's ThreadPool with
+    `threads` workers (CPU baseline sized to the host's CPU quota)."""
+    d = scene.desc()
+    h = image_height(cam)
+    out = np.zeros((h, cam.image_width, 3), dtype=np.float64)
+    bvh = scene.use_bvh if use_bvh is None else use_bvh
+    L = ref()
+    L.ref_trace_pool.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.CameraDesc), C.c_int,
+                                 C.c_int, C.POINTER(C.c_double)]
+    L.ref_trace_pool.restype = C.c_longlong
+    n = L.ref_trace_pool(C.byref(d), C.byref(cam), int(bvh), int(threads), dptr(out))
+    return n, out
+
+
+def ref_sample_batch(kind, seed, n):
+    L = ref()
+    L.ref_sample_batch.argtypes = [C.c_int, C.c_uint32, C.c_int, C.POINTER(C.c_double)]
+    out = np.zeros((n, 3))
+    assert L.ref_sample_batch(kind, seed, n, dptr(out)) == 0
+    return out
+
+
+def ref_light_batch(scene, org, seed, n, use_bvh=None):
+    L = ref()
+    L.ref_light_batch.argtypes = [C.POINTER(abi.SceneDesc), C.c_int, C.POINTER(C.c_double),
+                                  C.c_uint32, C.c_int, C.POINTER(C.c_double)]
+    d = scene.desc()
+    o = np.ascontiguousarray(org, dtype=np.float64)
+    out = np.zeros((n, 3))
+    bvh = scene.use_bvh if use_bvh is None else use_bvh
+    assert L.ref_light_batch(C.byref(d), int(bvh), dptr(o), seed, n, dptr(out)) == 0
+    return out
+
+
+def oracle_ctr_sample_batch(kind, seed, n):
+    L = oracle()
+    L.oracle_ctr_sample_batch.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    out = np.zeros((n, 3))
+    assert L.oracle_ctr_sample_batch(kind, seed, n, dptr(out)) == 0
+    return out
+
+
+def oracle_ctr_light_batch(scene, org, seed, n, use_bvh=None):
+    L = oracle()
+    L.oracle_ctr_light_batch.argtypes = [C.POINTER(abi.SceneDesc), C.c_int, C.POINTER(C.c_double),
+                                         C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    d = scene.desc()
+    o = np.ascontiguousarray(org, dtype=np.float64)
+    out = np.zeros((n, 3))
+    bvh = scene.use_bvh if use_bvh is None else use_bvh
+    assert L.oracle_ctr_light_batch(C.byref(d), int(bvh), dptr(o), seed, n, dptr(out)) == 0
+    return out
