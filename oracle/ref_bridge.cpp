@@ -379,6 +379,11 @@ int ref_object_hit(const rt_scene_desc *d, int obj, const double ray[7], double 
   int mi = -1;
   for (int k = 0; k < d->n_materials; ++k)
     if (g.mat[k] && g.mat[k] == rec.material) mi = k;
+  // ConstantMedium::hit never writes u, v (ConstantMedium.cpp:25-94): whatever
+  // the caller's -- or a HittableList's uninitialised temp -- record held stays.
+  // Store 0 for medium hits so the fixtures regenerate byte for byte.
+  for (int k = 0; k < d->n_objects; ++k)
+    if (d->objects[k].kind == RT_OBJ_MEDIUM && d->objects[k].phase == mi) rec.u = rec.v = 0.0;
   double v[12] = {rec.t,        rec.point.x(),  rec.point.y(),  rec.point.z(),
                   rec.normal.x(), rec.normal.y(), rec.normal.z(), rec.u,
                   rec.v,        rec.frontFace ? 1.0 : 0.0, (double)mi, 0};

@@ -206,20 +206,22 @@ def kats(var):
     return res
 
 
-def main():
+def main(out=HERE):
+    """Write the fixtures into `out` (default: this directory; the
+    reproducibility test writes them to a scratch directory and compares)."""
     if not O.ref_available():
         sys.exit("oracle/_ref/libref.so missing: run `make -C oracle ref` (needs /root/reference)")
     var = variants()
-    with open(os.path.join(HERE, "scene_variants.json"), "w") as f:
+    with open(os.path.join(out, "scene_variants.json"), "w") as f:
         json.dump({k: v for k, v in var.items() if k.startswith("bouncing_")}, f)
     arrays, meta = images(var)
-    np.savez_compressed(os.path.join(HERE, "ref_images.npz"), **arrays)
-    with open(os.path.join(HERE, "ref_images.json"), "w") as f:
+    np.savez_compressed(os.path.join(out, "ref_images.npz"), **arrays)
+    with open(os.path.join(out, "ref_images.json"), "w") as f:
         json.dump({"cases": meta, "seeds": SEEDS}, f, indent=1)
-    np.savez_compressed(os.path.join(HERE, "ref_ppm.npz"), **ppm_golden(var))
-    np.savez_compressed(os.path.join(HERE, "ref_kats.npz"), **kats(var))
-    print("goldens written to", HERE)
+    np.savez_compressed(os.path.join(out, "ref_ppm.npz"), **ppm_golden(var))
+    np.savez_compressed(os.path.join(out, "ref_kats.npz"), **kats(var))
+    print("goldens written to", out)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else HERE)

@@ -178,3 +178,21 @@ def test_counter_mode_statistically_matches_reference():
     ref_mean = np.mean([np.nanmean(O.oracle_render(S, cam, O.MODE_MT, s)) for s in (1, 2, 3)])
     ctr_mean = np.mean([np.nanmean(O.oracle_render(S, cam, O.MODE_COUNTER, s)) for s in (1, 2, 3)])
     assert abs(ref_mean - ctr_mean) / ref_mean < 0.05
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_goldens_regenerate_identically(tmp_path):
+    """make_goldens.py run again against the reference gives the committed
+    fixtures array for array (ConstantMedium's unset u, v are stored as 0)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "make_goldens", os.path.join(O.ROOT, "tests", "golden", "make_goldens.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    mg.main(str(tmp_path))
+    for f in ("ref_images", "ref_ppm", "ref_kats"):
+        a = np.load(os.path.join(O.ROOT, "tests", "golden", f + ".npz"))
+        b = np.load(os.path.join(str(tmp_path), f + ".npz"))
+        assert set(a.files) == set(b.files)
+        for k in a.files:
+            assert np.array_equal(a[k], b[k], equal_nan=True), (f, k)
