@@ -38,6 +38,7 @@
 #include "utils/ColorUtility.hpp"
 #include "utils/concurrency/ThreadPool.hpp"
 #include "ref_binding.hpp"
+#include "scene/Scene.hpp"
 #include "utils/math/Utility.hpp"
 #include "utils/math/Vec3Utility.hpp"
 
@@ -286,6 +287,40 @@ int ref_binding_roundtrip(const rt_scene_desc *d, rt_scene_desc *out) {
   root_lists(g, d, world, lights);
   builder.reset(new RtSceneBuilder());
   *out = builder->finish(world, lights, d->use_bvh != 0);
+  return 0;
+}
+
+/* The reference's own scene builders (main.cpp:21-131, compiled from the
+   reference's main.cpp text by oracle/Makefile) with the main-thread engine
+   seeded by `seed` (the bouncing scene draws its layout from it), converted by
+   INTEGRATION.md's binding.  which: 0 = populate_cornell_box_scene, 1 =
+   populate_bouncing_spheres_scene.  *cam gets the CameraConfig fields the
+   builder sets (CameraConfig.hpp defaults otherwise). */
+int ref_populate_scene(int which, uint32_t seed, rt_scene_desc *out, rt_camera_desc *cam) {
+  static std::unique_ptr<RtSceneBuilder> builder;
+  HittableList world, lights;
+  CameraConfig cfg;
+  random_engine().seed(seed);
+  if (which == 0)
+    populate_cornell_box_scene(world, lights, cfg);
+  else if (which == 1)
+    populate_bouncing_spheres_scene(world, lights, cfg);
+  else
+    return -1;
+  builder.reset(new RtSceneBuilder());
+  *out = builder->finish(world, lights, false);
+  cam->image_width = cfg.image_width;
+  cam->samples_per_pixel = cfg.samples_per_pixel;
+  cam->max_depth = cfg.max_depth;
+  cam->aspect_ratio = cfg.aspect_ratio;
+  cam->vfov = cfg.vfov;
+  cam->defocus_angle = cfg.defocus_angle;
+  cam->focus_dist = cfg.focus_dist;
+  auto cv = [](const Vec3 &v) { return rt_vec3{v.x(), v.y(), v.z()}; };
+  cam->lookfrom = cv(cfg.lookfrom);
+  cam->lookat = cv(cfg.lookat);
+  cam->vup = cv(cfg.vup);
+  cam->background = cv(cfg.background);
   return 0;
 }
 
