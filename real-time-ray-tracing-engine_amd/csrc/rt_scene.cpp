@@ -339,8 +339,19 @@ struct Compiler {
     return fail("unknown material kind");
   }
 
-  // Visit object o: compute its box (reference rules) and nesting depth.
+  // Visit object o: compute its box (reference rules) and nesting depth.  The
+  // recursion follows the wrapper/list nesting, bounded so that a deep chain in
+  // a caller's table cannot overflow the host stack (found by make sanitize).
+  static constexpr int kMaxNesting = 1000;
+  int nesting = 0;
+  struct NestGuard {
+    int &n;
+    explicit NestGuard(int &c) : n(c) { ++n; }
+    ~NestGuard() { --n; }
+  };
   bool visit(int o) {
+    NestGuard guard(nesting);
+    if (nesting > kMaxNesting) return fail("UNSUPPORTED: objects nested deeper than 1000 levels");
     if (o < 0 || o >= D->n_objects) return fail("object index out of range");
     if (state[o] == 2) return true;
     if (state[o] == 1) return fail("object graph has a cycle");

@@ -57,6 +57,17 @@ public:
 private:
   const std::string &s_;
   size_t i_ = 0;
+  // Nesting bound: value() recurses per array/object level, so an adversarial
+  // file ("[[[[...") would otherwise overflow the stack (found by make sanitize).
+  static constexpr int kMaxDepth = 256;
+  int depth_ = 0;
+  struct Nest {
+    Parser &p;
+    explicit Nest(Parser &q) : p(q) {
+      if (++p.depth_ > kMaxDepth) p.fail("nesting deeper than 256 levels");
+    }
+    ~Nest() { --p.depth_; }
+  };
 
   [[noreturn]] void fail(const std::string &m) {
     throw std::runtime_error("JSON parse error at offset " + std::to_string(i_) + ": " + m);
@@ -74,6 +85,7 @@ private:
     return false;
   }
   Value value() {
+    Nest guard(*this);
     ws();
     if (i_ >= s_.size()) fail("unexpected end");
     char c = s_[i_];

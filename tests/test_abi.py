@@ -128,3 +128,31 @@ def test_scene_json_errors():
     with pytest.raises(SceneError):
         load_scene({"materials": {"m": {"type": "lambertian", "texture": "nope"}},
                     "world": [{"type": "sphere", "center": [0, 0, 0], "radius": 1, "material": "m"}]})
+
+
+def test_deep_object_nesting_is_rejected_not_overflowing():
+    """A 5000-deep Translate chain in the caller's tables is refused by the scene
+    compiler's nesting bound (RT_ERR_UNSUPPORTED) instead of recursing 5000
+    frames deep (the bound `make sanitize` asked for)."""
+    n = 5000
+    objs = (abi.ObjectDesc * (n + 2))()
+    kids = (C.c_int32 * 1)(1)
+    objs[0].kind, objs[0].child, objs[0].count = abi.RT_OBJ_LIST, 0, 1
+    for k in range(1, n + 1):
+        objs[k].kind, objs[k].child = abi.RT_OBJ_TRANSLATE, k + 1
+        objs[k].a.x = 0.001
+    objs[n + 1].kind, objs[n + 1].material, objs[n + 1].s = abi.RT_OBJ_SPHERE, 0, 0.5
+    tex = (abi.TextureDesc * 1)()
+    tex[0].kind = abi.RT_TEX_SOLID
+    mats = (abi.MaterialDesc * 1)()
+    mats[0].kind, mats[0].texture = abi.RT_MAT_LAMBERTIAN, 0
+    d = abi.SceneDesc()
+    d.textures, d.n_textures = tex, 1
+    d.materials, d.n_materials = mats, 1
+    d.objects, d.n_objects = objs, n + 2
+    d.children, d.n_children = kids, 1
+    d.world, d.lights = 0, -1
+    L = load()
+    h = C.c_void_p()
+    assert L.rt_scene_create(C.byref(d), 0, C.byref(h)) == abi.RT_ERR_UNSUPPORTED
+    assert b"nested deeper" in L.rt_last_error()

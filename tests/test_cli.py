@@ -119,3 +119,23 @@ def test_cli_render_writes_reference_ppm(tmp_path):
     want = to_bytes(ref).astype(np.int64)
     assert np.abs(got - want).max() <= 1
     assert (got != want).mean() < 0.01
+
+
+CHECK = os.path.join(PKG, "build", "rtx_scene_check")
+
+
+@pytest.mark.skipif(not os.path.exists(CHECK), reason="build/rtx_scene_check not built")
+def test_scene_check_tool(tmp_path):
+    """rtx_scene_check runs the JSON loader + scene compiler + camera setup on
+    the host: every committed scene is valid; a 100k-deep JSON nesting is
+    rejected with a message (the parser's depth bound), not a stack overflow."""
+    r = subprocess.run([CHECK, *SCENES], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": ok ") == len(SCENES)
+    deep = tmp_path / "deep.json"
+    deep.write_text("[" * 100000 + "]" * 100000)
+    r = subprocess.run([CHECK, str(deep)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "nesting deeper than 256" in r.stdout
+    r = subprocess.run([CLI, "--scene", str(deep), "--dump-desc"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 1 and "nesting deeper" in r.stderr

@@ -22,7 +22,7 @@ NATIVE = os.path.join(os.path.dirname(__file__), "native")
 @pytest.fixture(scope="module")
 def emu():
     subprocess.run(["make", "-s", "-C", NATIVE], check=True)
-    L = C.CDLL(os.path.join(NATIVE, "build", "libemu.so"))
+    L = C.CDLL(os.environ.get("RTX_EMU_LIB", os.path.join(NATIVE, "build", "libemu.so")))
     L.emu_render.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.Frame),
                              C.POINTER(abi.RenderParams), C.c_int, C.POINTER(C.c_double)]
     return L
