@@ -103,6 +103,24 @@ def test_full_hd_rows_match_oracle():
     compare(gpu, ref)
 
 
+# BASELINE configs at their own sample counts, on bands of full-width rows the
+# threaded oracle can afford: C2 (spp 64), C3 (486-sphere BVH, defocus, motion
+# blur, glass; spp 256), C4 (Cornell + fog + Perlin + lights; spp 1024).
+BASELINE_BANDS = [("three_spheres", 64, (528, 544)), ("bouncing_seed42", 256, (516, 524)),
+                  ("cornell_fog", 1024, (698, 702))]
+
+
+@pytest.mark.parametrize("name,spp,rows", BASELINE_BANDS, ids=[b[0] for b in BASELINE_BANDS])
+def test_baseline_spp_bands_match_oracle(name, spp, rows):
+    S = scene(name)
+    cam = S.camera_desc(image_width=1920, samples_per_pixel=spp, max_depth=8)
+    f = camera_frame(cam)
+    with Renderer(S) as R:
+        gpu = R.render(f, seed=23, rows=rows)
+    ref = O.oracle_render(S, cam, O.MODE_COUNTER, 23, rows=rows, threads=16)
+    compare(gpu, ref)
+
+
 def test_spp_not_square_scales_by_spp():
     """spp=10 traces 3x3 strata but scales by 1/10 (StaticCamera.cpp:74-76, 98)."""
     S = scene("three_spheres")
