@@ -174,6 +174,19 @@ def host_cpu_info():
     return info
 
 
+def grow(run, target_s):
+    """Run run(spp) at square sample counts 1, 4, 9, ... (up to 256) until one
+    run takes at least half of target_s; returns (spp, seconds) of the last run.
+    Each step is sized from the previous run's rate, which per-row overhead
+    makes look slow at low spp."""
+    sq, dt = 1, run(1)
+    while dt < 0.5 * target_s and sq < 16:
+        nxt = int(sq * (target_s / max(dt, 1e-3)) ** 0.5)
+        sq = max(sq + 1, min(16, nxt))
+        dt = run(sq * sq)
+    return sq * sq, dt
+
+
 def cpu_baseline(scene, cam_full):
     """The reference's OWN multithreaded CPU path: StaticCamera::render with -p
     (use_parallelism), i.e. render_cpu's ThreadPool of
@@ -185,8 +198,8 @@ def cpu_baseline(scene, cam_full):
     1024-slot Chase-Lev deque overflows on rows wider than 1023 pixels and
     corrupts the heap -- measured: `malloc(): unaligned fastbin chunk detected`
     at 1920 wide, WorkStealingDeque.hpp:29-43 vs :72-85 -- so the sample keeps
-    rows short), with the stratum count chosen from a 1-spp calibration run so
-    the timed run is ~15 s of CPU work."""
+    rows short), at the square sample count grow() reaches from 1 spp for a
+    timed run of ~8-15 s of CPU work."""
     import ctypes as C
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -219,10 +232,7 @@ def cpu_baseline(scene, cam_full):
             os.chdir(cwd)
         return dt
 
-    t1 = run(1)
-    sq = max(1, min(16, int((15.0 / max(t1, 1e-3)) ** 0.5)))
-    spp = sq * sq
-    dt = run(spp) if spp > 1 else t1
+    spp, dt = grow(run, 15.0)
     n = width * h * spp
     out = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s",
            "cores": host["hardware_concurrency"],
@@ -239,20 +249,18 @@ def cpu_baseline(scene, cam_full):
     quota = host.get("cgroup_cpu_quota") or host.get("affinity_cpus")
     if O.ref_available() and quota and int(quota) < host["hardware_concurrency"]:
         nt = max(1, int(quota))
-        cam = scene.camera_desc(image_width=width, samples_per_pixel=1, max_depth=cam_full.max_depth)
-        t = time.perf_counter()
-        O.ref_trace_pool(scene, cam, nt)
-        t1 = time.perf_counter() - t
-        sq2 = max(1, min(16, int((10.0 / max(t1, 1e-3)) ** 0.5)))
-        cam = scene.camera_desc(image_width=width, samples_per_pixel=sq2 * sq2,
-                                max_depth=cam_full.max_depth)
-        t = time.perf_counter()
-        n2, _ = O.ref_trace_pool(scene, cam, nt)
-        dt2 = time.perf_counter() - t
+
+        def run_pool(spp):
+            cam = scene.camera_desc(image_width=width, samples_per_pixel=spp,
+                                    max_depth=cam_full.max_depth)
+            t = time.perf_counter()
+            O.ref_trace_pool(scene, cam, nt)
+            return time.perf_counter() - t
+        spp2, dt2 = grow(run_pool, 10.0)
         out["quota_sized_pool"] = {
-            "value": round(n2 / dt2 / 1e6, 4), "unit": "Msamples/s", "cores": nt,
+            "value": round(width * h * spp2 / dt2 / 1e6, 4), "unit": "Msamples/s", "cores": nt,
             "sample": "render_cpu -p loop on the reference ThreadPool with %d workers, "
-                      "%dx%d @ %d spp, %.1f s" % (nt, width, h, sq2 * sq2, dt2)}
+                      "%dx%d @ %d spp, %.1f s" % (nt, width, h, spp2, dt2)}
     return out
 
 
