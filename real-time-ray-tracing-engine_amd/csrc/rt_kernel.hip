@@ -44,14 +44,6 @@ using namespace rtp;
 #endif
 #define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : ((F) == 0 ? 16 : 1))
 #endif
-// Resumable BVH walks (rt_path.h trav_run): a wave stops walking to shade once
-// RT_SHADE_MIN lanes have finished theirs.
-#ifndef RT_RESUME
-#define RT_RESUME 1
-#endif
-#ifndef RT_SHADE_MIN
-#define RT_SHADE_MIN 32
-#endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
 #endif
@@ -113,10 +105,6 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   PathState ps;
   ps.active = false;
   Key key{P.seed_lo, P.seed_hi, 0, 0};
-  // BVH instances: walks resume across loop trips (rt_path.h trav_run)
-  constexpr bool kResume = RT_RESUME && (F & F_FLAT) == 0;
-  bool tracing = false;
-  Trav tv;
 
   for (;;) {
     // ---- regeneration: idle lanes pull the next (pixel, stratum) items
@@ -141,39 +129,13 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
           ps.T = v3(1.0, 1.0, 1.0);
           ps.bounce = 0;
           ps.active = C.max_depth > 0;
-          if constexpr (kResume) {
-            tracing = ps.active;
-            trav_begin(S, tv);
-          }
           if (STATS) n_samples++;
         }
       }
     }
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
-    if constexpr (kResume) {
-      trav_run<STATS, F>(S, ps.ray, tracing, ps.active, tv, stk, lnodes, cnt, RT_SHADE_MIN);
-      if (ps.active && !tracing) { // walk over: shade, then the next segment's walk
-        if (STATS) n_segments++;
-        Hit h;
-        bool cont;
-        if (trace_tail<STATS, F>(S, ps.ray, h, key, ps.bounce, tv.closest, tv.best, cnt)) {
-          cont = shade<STATS, F>(S, C, ps, key, h, cnt);
-        } else {
-          ps.T = ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
-          cont = false;
-        }
-        if (cont) {
-          tracing = true;
-          trav_begin(S, tv);
-        } else {
-          atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
-          atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
-          atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
-          ps.active = false;
-        }
-      }
-    } else if (ps.active) {
+    if (ps.active) {
       if (STATS) n_segments++;
       bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt);
       if (!cont) {

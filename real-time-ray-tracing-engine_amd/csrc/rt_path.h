@@ -874,148 +874,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   return trace_tail<STATS, F>(S, r, h, key, bounce, closest, best, cnt);
 }
 
-// ------------------------------------------------ resumable (dynamic-fetch) walk
-// trace() runs every lane's walk to completion, so a wave sits at the pace of
-// its longest walk: C3 measured 47 % useful lanes in the node loop.  The BVH
-// instances instead keep each lane's walk state across loop trips (Aila &
-// Laine 2009, "replacing terminated rays"): trav_run advances all unfinished
-// walks and returns as soon as `done_min` lanes have finished theirs; those
-// lanes shade and start their next segment (or a new camera path) from the
-// root while the others resume mid-tree.  The stack stays in LDS; between
-// trips a lane keeps only (cur, sp, lf, ln, best, closest) -- the per-ray slab
-// constants are recomputed from the unchanged ray on resume.  Same closest hit
-// as trace(): the walk and its culling bound are the same per lane.
-struct Trav {
-  int cur, sp, lf, ln; // next node (-1 none), stack depth, parked leaf range
-  int best;            // closest item so far (-1 none)
-  double closest;
-};
-
-RT_HD RT_FI void trav_begin(const DScene &S, Trav &t) {
-  t.sp = 0;
-  t.lf = 0;
-  t.ln = 0;
-  t.best = -1;
-  t.closest = kInf;
-  if (S.root_is_leaf) {
-    t.cur = -1;
-    t.ln = S.n_root_items;
-  } else {
-    t.cur = 0;
-  }
-}
-
-RT_HD RT_FI int wave_count(bool pred) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __popcll(__ballot(pred));
-#else
-  return pred ? 1 : 0;
-#endif
-}
-
-// Advance the walks of the lanes with `tracing` set; a lane whose walk ends
-// clears it.  Returns when no lane is tracing or `done_min` lanes of the wave
-// have `pending` set and `tracing` clear.
-template <bool STATS, unsigned F>
-RT_HD RT_FI void trav_run(const DScene &S, const Ray &r, bool &tracing, bool pending, Trav &t,
-                          int *stk, const RT_LDS DNode *lnodes, Counters &cnt, int done_min) {
-  static_assert((F & F_FLAT) == 0, "BVH instances only");
-  const double tmin = 0.001; // Camera.cpp:242
-  const double a = len2(r.d);
-  const double ya = RT_MK_SPHERE ? 1.0 / a : 0.0;
-  constexpr bool kFma = RT_SLAB_FMA;
-  const RayF<kFma> q = ray_f32<kFma>(r);
-  const float tmin32 = f32_dn(tmin);
-  float cl32 = f32_up(t.closest);
-  auto test_item = [&](int ii) {
-    if (STATS) cnt.wleaf += wave_once();
-    const DItem it = S.items[ii];
-    Ray lr = r;
-    double al = a;
-    const double *pya = &ya;
-    if constexpr ((F & F_XFORM) != 0) {
-      if (it.xf_count) {
-        lr = to_local(S, it.xf_first, it.xf_count, r);
-        al = len2(lr.d);
-        pya = nullptr;
-      }
-    }
-    double th;
-    bool hit;
-    if (it.kind == I_SPHERE) {
-      if (STATS) cnt.spheres++;
-      hit = sphere_root(S.spheres[it.idx], lr, al, tmin, t.closest, th, true, pya);
-    } else {
-      if (STATS) cnt.quads++;
-      hit = quad_t(S.quads[it.idx], lr, tmin, t.closest, th);
-    }
-    if (hit) {
-      t.closest = th;
-      cl32 = f32_up(th);
-      t.best = ii;
-    }
-  };
-  for (;;) {
-    // node loop of the walking lanes (while-while, postponed leaves: trace())
-    while (tracing && t.cur >= 0) {
-      if (STATS) cnt.wnode += wave_once();
-      if (wave_none(t.ln == 0)) break;
-      if (STATS) cnt.nodes++;
-      DNode N;
-      if (t.cur < S.n_lds_nodes) {
-        const RT_LDS DNode &L = lnodes[t.cur];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          N.lo0[k] = L.lo0[k];
-          N.hi0[k] = L.hi0[k];
-          N.lo1[k] = L.lo1[k];
-          N.hi1[k] = L.hi1[k];
-        }
-        N.entry[0] = L.entry[0];
-        N.entry[1] = L.entry[1];
-      } else {
-        N = S.nodes[t.cur];
-      }
-      const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
-      const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
-      const int e0 = N.entry[0], e1 = N.entry[1];
-      const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
-      if (h0 && h1) {
-        const bool first0 = tn0 <= tn1;
-        if (t.sp < S.stack_depth) stk[64 * t.sp++] = first0 ? e1 : e0;
-        t.cur = first0 ? e0 : e1;
-      } else if (h0 || h1) {
-        t.cur = h0 ? e0 : e1;
-      } else {
-        t.cur = t.sp > 0 ? stk[64 * --t.sp] : -1;
-      }
-      if (t.cur < -1 && t.ln == 0) {
-        t.lf = (~t.cur) >> 3;
-        t.ln = (~t.cur) & 7;
-        t.cur = t.sp > 0 ? stk[64 * --t.sp] : -1;
-      }
-    }
-    if (tracing) {
-      if (t.ln == 0) {
-        tracing = false; // nothing parked, nothing left to walk: the walk is over
-      } else {
-        while (t.ln > 0) { // ---- the single leaf-test site
-          const int ii = t.lf;
-          ++t.lf;
-          --t.ln;
-          test_item(ii);
-        }
-        if (t.cur < -1) {
-          t.lf = (~t.cur) >> 3;
-          t.ln = (~t.cur) & 7;
-          t.cur = t.sp > 0 ? stk[64 * --t.sp] : -1;
-        }
-      }
-    }
-    if (wave_none(tracing) || wave_count(pending && !tracing) >= done_min) return;
-  }
-}
-
 // ------------------------------------------------------------ lights
 // Sum over light leaves of weight * pdf_value (Plane.cpp:115-126, Sphere.cpp:145-158).
 template <bool STATS>
