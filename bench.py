@@ -108,7 +108,7 @@ def pmc_live(args):
         return None
     tmp = tempfile.mkdtemp(prefix="rtx_pmc_")
     child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2",
-             "--warmup", "1", "--no-cpu-baseline", "--pmc", "off"]
+             "--warmup", "1", "--no-cpu-baseline", "--pmc", "off", "--no-other-configs"]
     if args.width:
         child += ["--width", str(args.width)]
     if args.spp:
@@ -268,6 +268,44 @@ def scene_name_of(scene):
     return getattr(scene, "_name", "scene")
 
 
+def other_configs(args, torch, dev, skip):
+    """The other single-GPU BASELINE configs at their full size (C3: 486-sphere BVH
+    scene at spp 256; C4: Cornell + fog + Perlin at spp 1024), timed like the
+    headline (device-resident frame buffer, barrier-free single rank, K steps
+    bracketed by device syncs) so the bench line carries every 1080p config."""
+    from rtx import abi
+    from rtx.render import Renderer, camera_frame
+    from rtx.scene import load_scene
+    res = {}
+    for c in ("C3", "C4"):
+        if c == skip:
+            continue
+        name, width, spp, depth = CONFIGS[c]
+        S = load_scene(os.path.join(SCENES, name + ".json"))
+        f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
+        buf = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
+        steps = 2 if c == "C4" else 4
+        with Renderer(S, device=dev.index or 0) as R:
+            def go(seed):
+                R.render_device(f, buf.data_ptr(), 0, seed=seed, output=abi.RT_OUT_SUM, accumulate=0)
+            go(999)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            ms = []
+            for k in range(steps):
+                go(k)
+                ms.append(R.last_kernel_ms())
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+        n = f.image_width * f.image_height * f.sqrt_spp ** 2 * steps
+        res[c] = {"workload": "%s %s %dx%d spp%d depth%d" % (c, name, f.image_width, f.image_height,
+                                                             f.sqrt_spp ** 2, depth),
+                  "value": round(n / dt / 1e6, 3), "unit": "Msamples/s", "steps": steps,
+                  "ms_per_step": round(dt * 1e3 / steps, 3),
+                  "kernel_ms": round(sum(ms) / len(ms), 3)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,6 +315,8 @@ def main():
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="N=1: skip timing C3 and C4 beside the headline config")
     # rehearsal of the N>1 path on one GPU: every rank on cuda:0, gloo all_reduce
     # instead of RCCL reduce (the driver's 8-GPU runs use the defaults)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
@@ -522,6 +562,8 @@ def main():
     }
     if check is not None:
         out["check"] = check
+    if rank == 0 and ws == 1 and not args.no_other_configs and not args.width and not args.spp:
+        out["other_configs"] = other_configs(args, torch, dev, args.config)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, cam)
     if rank == 0:

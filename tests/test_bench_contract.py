@@ -20,7 +20,7 @@ KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
 
 def _bench(*extra, timeout=110):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C1", "--steps", "2",
-           "--warmup", "1", "--no-cpu-baseline", "--check", *extra]
+           "--warmup", "1", "--no-cpu-baseline", "--no-other-configs", "--check", *extra]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
