@@ -160,14 +160,16 @@ typedef struct rt_scene_desc {
   int32_t use_bvh; /* reference -b: lights become HittableList(BVHNode(lights))
                       (StaticCamera.cpp:35-40); the world is always traversed through
                       the library's own BVH (closest hit is structure independent) */
-  int32_t bvh_builder; /* RT_BVH_AUTO (0): device LBVH from 65536 world primitives,
-                          host SAH below; RT_BVH_HOST; RT_BVH_DEVICE */
+  int32_t bvh_builder; /* RT_BVH_AUTO (0): device binned SAH from 65536 world
+                          primitives, host SAH below; RT_BVH_HOST; RT_BVH_DEVICE
+                          (linear BVH); RT_BVH_DEVICE_SAH */
 } rt_scene_desc;
 
 enum {
   RT_BVH_AUTO = 0,
   RT_BVH_HOST = 1,  /* binned SAH on the host (rt_scene.cpp) */
-  RT_BVH_DEVICE = 2 /* linear BVH on the GPU (rt_bvh_build.hip) */
+  RT_BVH_DEVICE = 2, /* linear BVH on the GPU (rt_bvh_build.hip) */
+  RT_BVH_DEVICE_SAH = 3 /* binned SAH on the GPU, level by level (rt_bvh_sah.hip) */
 };
 
 /* ---- camera (CameraConfig.hpp:9-35) ------------------------------------- */
@@ -270,7 +272,8 @@ typedef struct rt_scene_info {
   int64_t device_bytes; /* total device bytes of the scene */
   int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise */
   int32_t lds_nodes;    /* BVH nodes (BFS prefix) the kernel stages in LDS per block */
-  int32_t bvh_builder;  /* the builder that made the world BVH: RT_BVH_HOST / RT_BVH_DEVICE */
+  int32_t bvh_builder;  /* the builder that made the world BVH: RT_BVH_HOST / RT_BVH_DEVICE /
+                           RT_BVH_DEVICE_SAH */
   int32_t _pad;
 } rt_scene_info;
 
@@ -298,6 +301,13 @@ int rt_render(rt_scene *scene, const rt_frame *frame, const rt_render_params *pa
 int rt_render_device(rt_scene *scene, const rt_frame *frame,
                      const rt_render_params *params, double *device_rgb,
                      void *hip_stream);
+
+/* SAH cost of the world BVH, relative to the root box: 1 (the root) + the sum
+   over every node's two children of area(child) / area(root) x (leaf: its item
+   count; inner: 1) -- the tree-quality figure of the reference's builder
+   (BVHNode.cpp:215-254, unit traversal and intersection costs).  0 for a flat
+   world.  Copies the nodes back from the device. */
+int rt_scene_bvh_cost(const rt_scene *scene, double *cost);
 
 /* Run the counter-instrumented kernel variant (untimed) and return totals. */
 int rt_render_stats(rt_scene *scene, const rt_frame *frame,

@@ -8,6 +8,7 @@
 // across the ABI: they return a negative code and set a thread-local message.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +27,11 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
 extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
                                       int *waves_per_simd);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
+extern "C" size_t rtk_sah_temp_bytes(int n);
+extern "C" hipError_t rtk_build_sah(const double *boxes, const DItem *items_in, int n,
+                                    DNode *nodes, DItem *items_out, void *temp,
+                                    size_t temp_bytes, int stack_budget, int *n_nodes,
+                                    int *depth, int *root_leaf, hipStream_t st);
 extern "C" hipError_t rtk_build_lbvh(const double *boxes, const DItem *items_in, int n,
                                      const double *scene_lo, const double *scene_hi,
                                      DNode *nodes, DItem *items_out, int *depth_dev, void *temp,
@@ -187,14 +193,26 @@ int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame) {
   return RT_OK;
 }
 
-// Runs rtk_build_lbvh over the scene's world items (uploaded in scene order at
-// `items`): writes the nodes and the items in leaf order in place.
+// Builds the world BVH on the device over the scene's world items (uploaded in
+// scene order at `items`): the binned-SAH builder (rt_bvh_sah.hip) or the linear
+// BVH (rt_bvh_build.hip); writes the nodes and the items in leaf order in place.
+// Depth at which the device SAH builder switches to balanced splits (the host
+// builder's force_median bound); RTX_SAH_STACK_BUDGET lowers it in tests.
+static int sah_stack_budget() {
+  int b = RT_STACK_DEPTH - 2;
+  if (const char *v = std::getenv("RTX_SAH_STACK_BUDGET")) b = std::max(1, std::min(b, std::atoi(v)));
+  return b;
+}
+struct DeviceTree {
+  int n_nodes = 0, depth = -1, root_leaf = 0;
+};
 static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *nodes,
-                                   DItem *items, int *depth) {
+                                   DItem *items, DeviceTree &tree) {
   const int n = (int)H.items.size();
+  const bool sah = H.device_bvh == RT_BVH_DEVICE_SAH;
   const size_t a_box = (6 * sizeof(double) * n + 255) & ~size_t(255);
   const size_t a_items = (sizeof(DItem) * n + 255) & ~size_t(255);
-  const size_t lb = rtk_lbvh_temp_bytes(n);
+  const size_t lb = sah ? rtk_sah_temp_bytes(n) : rtk_lbvh_temp_bytes(n);
   const size_t total = a_box + a_items + 256 + lb;
   char *tmp = nullptr;
   hipError_t e = hipMalloc((void **)&tmp, total);
@@ -205,13 +223,20 @@ static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *
   void *d_lb = tmp + a_box + a_items + 256;
   e = hipMemcpyAsync(d_box, H.item_boxes.data(), 6 * sizeof(double) * n, hipMemcpyHostToDevice,
                      s->stream);
-  if (e == hipSuccess)
-    e = rtk_build_lbvh(d_box, items, n, H.scene_lo, H.scene_hi, nodes, d_sorted, d_depth, d_lb, lb,
-                       s->stream);
+  if (sah) {
+    if (e == hipSuccess)
+      e = rtk_build_sah(d_box, items, n, nodes, d_sorted, d_lb, lb, sah_stack_budget(),
+                        &tree.n_nodes, &tree.depth, &tree.root_leaf, s->stream);
+  } else {
+    tree.n_nodes = n - 1;
+    if (e == hipSuccess)
+      e = rtk_build_lbvh(d_box, items, n, H.scene_lo, H.scene_hi, nodes, d_sorted, d_depth, d_lb,
+                         lb, s->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(&tree.depth, d_depth, sizeof(int), hipMemcpyDeviceToHost, s->stream);
+  }
   if (e == hipSuccess)
     e = hipMemcpyAsync(items, d_sorted, sizeof(DItem) * n, hipMemcpyDeviceToDevice, s->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(depth, d_depth, sizeof(int), hipMemcpyDeviceToHost, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   (void)hipFree(tmp);
   return e;
@@ -319,17 +344,20 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   // tree is deeper than the traversal stack
   int builder = RT_BVH_HOST;
   if (H.device_bvh) {
-    int depth = -1;
-    hipError_t be = device_bvh_build(s, H, (DNode *)P(iN), (DItem *)P(iI), &depth);
+    DeviceTree tree;
+    hipError_t be = device_bvh_build(s, H, (DNode *)P(iN), (DItem *)P(iI), tree);
     if (be != hipSuccess) {
       rt_scene_destroy(s);
       return hip_err(be, "device BVH build");
     }
     int max_depth = RT_STACK_DEPTH - 1;
     if (const char *md = std::getenv("RTX_LBVH_MAX_DEPTH")) max_depth = std::atoi(md); // tests
-    if (depth >= 0 && depth <= max_depth) {
-      H.bvh_depth = depth;
-      builder = RT_BVH_DEVICE;
+    if (tree.depth >= 0 && tree.depth <= max_depth) {
+      H.bvh_depth = tree.depth;
+      H.nodes.resize(tree.n_nodes); // the device arrays hold the tree; sizes only
+      H.root_is_leaf = tree.root_leaf > 0;
+      H.n_root_items = tree.root_leaf;
+      builder = H.device_bvh;
     } else { // too deep for the per-lane stack: rebuild on the host (depth-capped SAH)
       rtx::build_world_bvh_host(H);
       hipError_t ue = hipMemcpy((void *)P(iN), H.nodes.data(), H.nodes.size() * sizeof(DNode),
@@ -533,6 +561,37 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->wave_node_iters = h[9];
   stats->wave_leaf_iters = h[10];
   stats->wave_shade_iters = h[11];
+  return RT_OK;
+}
+
+int rt_scene_bvh_cost(const rt_scene *s, double *cost) {
+  if (!s || !cost) return set_err(RT_ERR_INVALID, "null argument");
+  *cost = 0.0;
+  const int n = s->ds.n_nodes;
+  if (s->ds.root_is_leaf || n <= 0) return RT_OK;
+  std::vector<DNode> nodes(n);
+  DeviceGuard g(s->device);
+  hipError_t e = hipMemcpy(nodes.data(), s->ds.nodes, sizeof(DNode) * n, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_err(e, "hipMemcpy nodes");
+  auto area = [](const float *lo, const float *hi) {
+    const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+    return 2.0 * (x * y + y * z + z * x);
+  };
+  float rlo[3], rhi[3];
+  for (int a = 0; a < 3; ++a) {
+    rlo[a] = std::min(nodes[0].lo0[a], nodes[0].lo1[a]);
+    rhi[a] = std::max(nodes[0].hi0[a], nodes[0].hi1[a]);
+  }
+  const double root = area(rlo, rhi);
+  if (!(root > 0.0)) return RT_OK;
+  double c = 1.0;
+  for (const DNode &d : nodes)
+    for (int k = 0; k < 2; ++k) {
+      const int e = d.entry[k];
+      const double w = e >= 0 ? 1.0 : (double)((~e) & 7);
+      c += w * area(k ? d.lo1 : d.lo0, k ? d.hi1 : d.hi0) / root;
+    }
+  *cost = c;
   return RT_OK;
 }
 

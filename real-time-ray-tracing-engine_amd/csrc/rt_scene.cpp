@@ -894,10 +894,10 @@ struct Compiler {
     emit_materials();
     const int builder = D->bvh_builder;
     const bool device = ibox.size() >= 2 &&
-                        (builder == RT_BVH_DEVICE ||
+                        (builder == RT_BVH_DEVICE || builder == RT_BVH_DEVICE_SAH ||
                          (builder == RT_BVH_AUTO && ibox.size() >= (size_t)kDeviceBuildMin));
-    if (device) { // built by the library on the GPU after upload (rt_bvh_build.hip)
-      H.device_bvh = 1;
+    if (device) { // built by the library on the GPU after upload (rt_bvh_sah.hip / rt_bvh_build.hip)
+      H.device_bvh = builder == RT_BVH_DEVICE ? RT_BVH_DEVICE : RT_BVH_DEVICE_SAH;
       H.item_boxes.reserve(6 * ibox.size());
       for (int a = 0; a < 3; ++a) {
         H.scene_lo[a] = kInf;

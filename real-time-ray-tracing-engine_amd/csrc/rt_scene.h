@@ -26,8 +26,10 @@ struct HostScene {
   int32_t root_is_leaf = 0;
   int32_t n_root_items = 0;
   int32_t bvh_depth = 0;
-  // device-built world BVH (rt_bvh_build.hip): items still in scene order, their
-  // boxes (lo xyz, hi xyz) and the centroid bounds; nodes sized, not filled
+  // device-built world BVH (0: built on the host; RT_BVH_DEVICE: linear BVH,
+  // rt_bvh_build.hip; RT_BVH_DEVICE_SAH: binned SAH, rt_bvh_sah.hip): items still
+  // in scene order, their boxes (lo xyz, hi xyz) and the centroid bounds; nodes
+  // sized, not filled
   int32_t device_bvh = 0;
   std::vector<double> item_boxes;
   double scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};

@@ -63,7 +63,7 @@ class SceneDesc(C.Structure):
                 ("bvh_builder", C.c_int32)]
 
 
-RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE = 0, 1, 2
+RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
 
 
 class CameraDesc(C.Structure):
@@ -118,4 +118,5 @@ EXPORTS = (
     "rt_scene_create", "rt_scene_info_get", "rt_scene_destroy", "rt_render",
     "rt_render_device", "rt_render_stats", "rt_last_kernel_ms", "rt_to_bytes_device",
     "rt_multi_create", "rt_multi_render", "rt_multi_shard_ms", "rt_multi_destroy",
+    "rt_scene_bvh_cost",
 )

@@ -54,6 +54,7 @@ def load():
     L.rt_multi_render.argtypes = [C.c_void_p, P(abi.Frame), P(abi.RenderParams), P(C.c_double)]
     L.rt_multi_shard_ms.argtypes = [C.c_void_p, P(C.c_double)]
     L.rt_multi_destroy.argtypes = [C.c_void_p]
+    L.rt_scene_bvh_cost.argtypes = [C.c_void_p, P(C.c_double)]
     for name in abi.EXPORTS:
         getattr(L, name).restype = C.c_char_p if name == "rt_last_error" else C.c_int
     if L.rt_abi_version() != 1:

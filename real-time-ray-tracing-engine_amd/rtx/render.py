@@ -115,6 +115,12 @@ class Renderer:
         check(self.lib.rt_render_stats(self.handle, C.byref(frame), C.byref(p), C.byref(s)))
         return {k: getattr(s, k) for k, _ in abi.PathStats._fields_}
 
+    def bvh_cost(self):
+        """SAH cost of the world BVH relative to the root box (rt_scene_bvh_cost)."""
+        c = C.c_double()
+        check(self.lib.rt_scene_bvh_cost(self.handle, C.byref(c)))
+        return c.value
+
     def last_kernel_ms(self):
         ms = C.c_double()
         check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))

@@ -1,7 +1,9 @@
-"""World BVH built on the GPU (rt_bvh_build.hip): the linear
-BVH gives the same images as the host SAH tree (the closest hit does not depend
-on the tree), matches the oracle, and falls back to the host build when the
-tree is deeper than the traversal stack."""
+"""World BVH built on the GPU: the binned-SAH builder
+(rt_bvh_sah.hip) and the linear BVH (rt_bvh_build.hip) give the same images as
+the host SAH tree (the closest hit does not depend on the tree), match the
+oracle, the SAH tree's cost stays within a few percent of the host SAH tree's,
+balanced splits keep it inside the traversal stack, and a tree deeper than the
+stack falls back to the host build."""
 import os
 
 import numpy as np
@@ -21,6 +23,9 @@ def compare(a, b, tol):
     np.testing.assert_allclose(np.nan_to_num(a), np.nan_to_num(b), rtol=0, atol=tol)
 
 
+DEVICE = (abi.RT_BVH_DEVICE, abi.RT_BVH_DEVICE_SAH)
+
+
 @pytest.mark.parametrize("name,w,spp", [("bouncing_seed42", 48, 4), ("cornell_fog", 32, 9),
                                         ("cornell", 32, 4)])
 def test_device_bvh_matches_oracle_and_host_tree(name, w, spp):
@@ -28,14 +33,16 @@ def test_device_bvh_matches_oracle_and_host_tree(name, w, spp):
     cam = S.camera_desc(image_width=w, samples_per_pixel=spp, max_depth=8)
     f = camera_frame(cam)
     out = {}
-    for b in (abi.RT_BVH_HOST, abi.RT_BVH_DEVICE):
+    for b in (abi.RT_BVH_HOST,) + DEVICE:
         S.bvh_builder = b
         with Renderer(S) as R:
             info = R.info()
             assert info["bvh_builder"] == b
             out[b] = R.render(f, seed=9)
-    compare(out[abi.RT_BVH_DEVICE], O.oracle_render(S, cam, O.MODE_COUNTER, 9), 1e-4)
-    compare(out[abi.RT_BVH_DEVICE], out[abi.RT_BVH_HOST], 1e-12)
+    ref = O.oracle_render(S, cam, O.MODE_COUNTER, 9)
+    for b in DEVICE:
+        compare(out[b], ref, 1e-4)
+        compare(out[b], out[abi.RT_BVH_HOST], 1e-12)
 
 
 def random_spheres(n, seed=1):
@@ -58,7 +65,7 @@ def test_auto_builder_uses_device_for_large_scenes():
     cam = S.camera_desc(image_width=48, samples_per_pixel=4, max_depth=6)
     f = camera_frame(cam)
     with Renderer(S) as R:
-        assert R.info()["bvh_builder"] == abi.RT_BVH_DEVICE
+        assert R.info()["bvh_builder"] == abi.RT_BVH_DEVICE_SAH
         dev = R.render(f, seed=2)
     S.bvh_builder = abi.RT_BVH_HOST
     with Renderer(S) as R:
@@ -76,3 +83,46 @@ def test_too_deep_device_tree_falls_back_to_host(monkeypatch):
         assert R.info()["bvh_builder"] == abi.RT_BVH_HOST
         img = R.render(camera_frame(cam), seed=9)
     compare(img, O.oracle_render(S, cam, O.MODE_COUNTER, 9), 1e-4)
+
+
+def test_device_sah_tree_quality_and_images():
+    """100k random spheres: the device binned-SAH tree costs within 10 % of the
+    host SAH tree (rt_scene_bvh_cost), the linear BVH's cost is reported beside
+    it, and all three trees give the same image."""
+    S = load_scene(random_spheres(100000, seed=3))
+    cam = S.camera_desc(image_width=64, samples_per_pixel=4, max_depth=6)
+    f = camera_frame(cam)
+    cost, img, info = {}, {}, {}
+    for b in (abi.RT_BVH_HOST, abi.RT_BVH_DEVICE, abi.RT_BVH_DEVICE_SAH):
+        S.bvh_builder = b
+        with Renderer(S) as R:
+            info[b] = R.info()
+            assert info[b]["bvh_builder"] == b
+            cost[b] = R.bvh_cost()
+            img[b] = R.render(f, seed=4)
+    assert cost[abi.RT_BVH_HOST] > 1
+    assert cost[abi.RT_BVH_DEVICE_SAH] <= 1.10 * cost[abi.RT_BVH_HOST], cost
+    assert info[abi.RT_BVH_DEVICE_SAH]["bvh_depth"] < 32
+    for b in DEVICE:
+        compare(img[b], img[abi.RT_BVH_HOST], 1e-12)
+
+
+def test_device_sah_depth_budget_balanced_splits(monkeypatch):
+    """With the stack budget lowered to 8 levels, the device SAH builder switches
+    to balanced (count-median) splits below it: the tree stays shallow and the
+    image is unchanged."""
+    monkeypatch.setenv("RTX_SAH_STACK_BUDGET", "8")
+    S = load_scene(random_spheres(20000, seed=5))
+    S.bvh_builder = abi.RT_BVH_DEVICE_SAH
+    cam = S.camera_desc(image_width=48, samples_per_pixel=4, max_depth=6)
+    f = camera_frame(cam)
+    with Renderer(S) as R:
+        info = R.info()
+        assert info["bvh_builder"] == abi.RT_BVH_DEVICE_SAH
+        assert info["bvh_depth"] <= 20, info  # ~log2(20000 / 2) = 14 for exact halves
+        dev = R.render(f, seed=6)
+    monkeypatch.delenv("RTX_SAH_STACK_BUDGET")
+    S.bvh_builder = abi.RT_BVH_HOST
+    with Renderer(S) as R:
+        host = R.render(f, seed=6)
+    compare(dev, host, 1e-12)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""World-BVH build: host binned SAH vs device LBVH (rt_bvh_build.hip).
+"""World-BVH build: host binned SAH vs device LBVH (rt_bvh_build.hip) vs device
+binned SAH (rt_bvh_sah.hip).
 
 For N random spheres: rt_scene_create time (compile + upload + build) with each
 builder, the tree depth, and the render rate through each tree (1920x1080,
@@ -45,7 +46,7 @@ def main():
         cam = S.camera_desc(image_width=1920, samples_per_pixel=4, max_depth=8)
         f = camera_frame(cam)
         buf = torch.zeros((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda")
-        for b in (abi.RT_BVH_HOST, abi.RT_BVH_DEVICE):
+        for b in (abi.RT_BVH_HOST, abi.RT_BVH_DEVICE, abi.RT_BVH_DEVICE_SAH):
             S.bvh_builder = b
             S.desc()
             torch.cuda.synchronize()
@@ -60,10 +61,13 @@ def main():
                 R.render_device(f, buf.data_ptr(), 0, seed=2 + k, output=abi.RT_OUT_SUM, accumulate=0)
                 torch.cuda.synchronize()
                 ms.append(R.last_kernel_ms())
+            cost = R.bvh_cost()
             R.close()
-            print(json.dumps({"n": n, "builder": "host_sah" if b == abi.RT_BVH_HOST else "device_lbvh",
+            name = {abi.RT_BVH_HOST: "host_sah", abi.RT_BVH_DEVICE: "device_lbvh",
+                    abi.RT_BVH_DEVICE_SAH: "device_sah"}[b]
+            print(json.dumps({"n": n, "builder": name, "built_by": info["bvh_builder"],
                               "create_s": round(t_create, 4), "bvh_depth": info["bvh_depth"],
-                              "nodes": info["n_nodes"],
+                              "nodes": info["n_nodes"], "sah_cost": round(cost, 2),
                               "render_Msamples_s": round(f.image_width * f.image_height * 4 / min(ms) / 1e3, 1)}),
                   flush=True)
 
