@@ -527,6 +527,10 @@ def main():
                             "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
                             "gbs": round(achieved, 1)}
     roof["counters"] = st
+    if st.get("cyc_loop"):
+        # STATS instance: shares of a wavefront's loop time per region (s_memtime)
+        roof["phase_share"] = {k[4:]: round(st[k] / st["cyc_loop"], 4) for k in (
+            "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights")}
     roof["lane_utilisation"] = {
         "traversal": round(st["node_visits"] / max(1, 64 * st["wave_node_iters"]), 4),
         "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),

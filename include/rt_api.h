@@ -259,6 +259,13 @@ typedef struct rt_path_stats {
   uint64_t wave_node_iters; /* traversal node-loop iterations */
   uint64_t wave_leaf_iters; /* leaf-item loop iterations */
   uint64_t wave_shade_iters; /* shading branch executions (lambertian/metal/dielectric/light) */
+  /* Where a wavefront's time goes: shader cycles (s_memtime) summed over
+     wavefronts, each region counted once per wave visit -- the loop overall,
+     camera-ray regeneration, closest-hit queries (traversal + items + media +
+     record), the media part of them, material shading, light sampling + light
+     pdf, texture evaluation.  Instrumentation adds a few percent; the shares
+     are what matters. */
+  uint64_t cyc_loop, cyc_regen, cyc_trace, cyc_media, cyc_shade, cyc_lights;
 } rt_path_stats;
 
 typedef struct rt_scene_info {

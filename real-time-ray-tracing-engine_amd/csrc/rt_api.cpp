@@ -561,6 +561,12 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->wave_node_iters = h[9];
   stats->wave_leaf_iters = h[10];
   stats->wave_shade_iters = h[11];
+  stats->cyc_loop = h[12];
+  stats->cyc_regen = h[13];
+  stats->cyc_trace = h[14];
+  stats->cyc_media = h[15];
+  stats->cyc_shade = h[16];
+  stats->cyc_lights = h[17];
   return RT_OK;
 }
 

@@ -97,7 +97,9 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   acc[lane * 3 + 1] = 0.0;
   acc[lane * 3 + 2] = 0.0;
 
-  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t cyc_regen = 0;
+  const uint64_t t_start = STATS ? clk() : 0;
   uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
 
   const int n_items = 64 * max(0, s_count);
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
 
   for (;;) {
     // ---- regeneration: idle lanes pull the next (pixel, stratum) items
+    const uint64_t t_regen = STATS ? clk() : 0;
     for (;;) {
       unsigned long long idle = __ballot(!ps.active);
       if (idle == 0 || next_item >= n_items) break;
@@ -133,6 +136,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
         }
       }
     }
+    if (STATS) cyc_regen += clk() - t_regen; // converged here (every lane)
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
@@ -172,9 +176,12 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     }
   }
   if (STATS) {
+    const uint64_t cyc_loop = clk() - t_start;
     unsigned long long v[RT_N_STATS] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
                                         cnt.quads, cnt.other,  cnt.light, cnt.shade,
-                                        lane == 0 ? n_trips : 0u, cnt.wnode, cnt.wleaf, cnt.wshade};
+                                        lane == 0 ? n_trips : 0u, cnt.wnode, cnt.wleaf, cnt.wshade,
+                                        lane == 0 ? cyc_loop : 0u, lane == 0 ? cyc_regen : 0u,
+                                        cnt.ctrace, cnt.cmedia, cnt.cshade, cnt.clights};
     for (int k = 0; k < RT_N_STATS; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);

@@ -26,7 +26,7 @@
 #include <stdint.h>
 
 #define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
-#define RT_N_STATS 12      // counters of the STATS kernel instance (rt_path_stats)
+#define RT_N_STATS 18      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 #ifndef RT_FLAT_MAX
 #define RT_FLAT_MAX 8 // worlds of at most this many items are one flat leaf (no BVH walk)

@@ -669,7 +669,16 @@ RT_HD RT_FI float slab(const RayF<FMA> &q, const float *lo, const float *hi, flo
 struct Counters {
   uint32_t nodes, spheres, quads, other, light, shade;
   uint32_t wnode, wleaf, wshade; // wave-level iterations (counted by one lane per wave)
+  uint64_t ctrace, cmedia, cshade, clights; // wave-level cycles (first active lane adds)
 };
+// shader clock for the STATS instance's phase cycles (s_memtime)
+RT_HD RT_FI uint64_t clk() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_readcyclecounter();
+#else
+  return 0;
+#endif
+}
 // true when no active lane of the wavefront has `pred` (a single-lane host build: !pred)
 RT_HD RT_FI bool wave_none(bool pred) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -701,6 +710,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
   const bool moving = kFlat ? !S.static_spheres : true;
   bool best_full = false;
   if constexpr ((F & F_MEDIA) != 0) {
+    const uint64_t t0 = STATS ? clk() : 0;
     constexpr bool kFma = RT_SLAB_FMA && !kFlat;
     const RayF<kFma> q = ray_f32<kFma>(r);
     const float tmin32 = f32_dn(tmin);
@@ -718,6 +728,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
         h = tmp;
       }
     }
+    if (STATS && wave_once()) cnt.cmedia += clk() - t0;
   }
   if (best < 0) return false;
   if (!best_full) {
@@ -1049,8 +1060,10 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   bool from_light = false;
   if constexpr ((F & F_LIGHTS) != 0) {
     if (e0 < 0.5 && have_lights) {
+      const uint64_t t0 = STATS ? clk() : 0;
       gd = lights_random(S, h.p, e1, d0, d1);
       from_light = true;
+      if (STATS && wave_once()) cnt.clights += clk() - t0;
     }
   }
   if (!from_light) {
@@ -1077,7 +1090,11 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   }
   double p0 = mat_pdf;
   if constexpr ((F & F_LIGHTS) != 0) {
-    if (have_lights) p0 = lights_pdf<STATS>(S, h.p, gd, cnt);
+    if (have_lights) {
+      const uint64_t t0 = STATS ? clk() : 0;
+      p0 = lights_pdf<STATS>(S, h.p, gd, cnt);
+      if (STATS && wave_once()) cnt.clights += clk() - t0;
+    }
   }
   double pdf = 0.5 * p0 + 0.5 * mat_pdf;
   double spdf;
@@ -1103,11 +1120,17 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
                                         const Key &key, int *stk, const RT_LDS DNode *lnodes,
                                         Counters &cnt) {
   Hit h;
-  if (!trace<STATS, F>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt)) {
+  const uint64_t t0 = STATS ? clk() : 0;
+  const bool hit = trace<STATS, F>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt);
+  const uint64_t t1 = STATS ? clk() : 0;
+  if (STATS && wave_once()) cnt.ctrace += t1 - t0;
+  if (!hit) {
     ps.T = ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
     return false;
   }
-  return shade<STATS, F>(S, C, ps, key, h, cnt);
+  const bool cont = shade<STATS, F>(S, C, ps, key, h, cnt);
+  if (STATS && wave_once()) cnt.cshade += clk() - t1;
+  return cont;
 }
 
 template <bool KB = false> // KB: philox10

@@ -99,7 +99,8 @@ class PathStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "samples", "segments", "node_visits", "sphere_tests", "quad_tests",
         "other_tests", "light_tests", "shade_events",
-        "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters")]
+        "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters",
+        "cyc_loop", "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights")]
 
 
 class SceneInfo(C.Structure):

@@ -24,7 +24,7 @@ namespace {
 template <unsigned F>
 void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, int i, int j,
                  int s0, int s1, int *stk, double acc[3]) {
-  Counters cnt{0, 0, 0, 0, 0, 0};
+  Counters cnt{};
   for (int k = s0; k < s1; ++k) {
     Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)(j * C.W + i), (uint32_t)k};
     PathState ps;
