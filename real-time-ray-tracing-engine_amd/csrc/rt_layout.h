@@ -68,8 +68,13 @@ struct DQuad {       // 144 B — Plane.hpp members
   double w[3];       // n / (n.n)
   double D;
   double area;
-  double pad;
+  int32_t aa;        // axis-aligned quad (u, v, n and w each on one axis; make_box's
+                     // faces, the Cornell walls): k | i << 2 | j << 4 | neg << 6 with
+                     // k the normal axis, i / j the u / v axes, neg = the permutation
+                     // (k, i, j) is odd; -1 otherwise (rt_path.h quad_t)
+  int32_t pad_;
 };
+static_assert(sizeof(DQuad) == 144, "DQuad layout");
 
 struct DMedium {     // ConstantMedium: -1/density, phase material, boundary items
   double neg_inv_density;

@@ -559,6 +559,23 @@ struct Compiler {
     }
     q.D = dotp(nn, Q);
     q.area = len;
+    // axis-aligned: every vector with one nonzero component, on three distinct axes
+    auto axis = [](const double a[3]) {
+      int k = -1, nz = 0;
+      for (int c = 0; c < 3; ++c)
+        if (a[c] != 0.0) {
+          k = c;
+          ++nz;
+        }
+      return nz == 1 && std::isfinite(a[k]) ? k : -1;
+    };
+    const int ak = axis(na), ai = axis(ua), aj = axis(va), aw = axis(wa);
+    q.aa = -1;
+    if (ak >= 0 && ai >= 0 && aj >= 0 && aw == ak && ak != ai && ak != aj && ai != aj &&
+        std::isfinite(q.D) && std::isfinite(Qa[0]) && std::isfinite(Qa[1]) && std::isfinite(Qa[2])) {
+      const bool even = (ak + 1) % 3 == ai; // (k, i, j) a cyclic shift of (0, 1, 2)
+      q.aa = ak | (ai << 2) | (aj << 4) | ((even ? 0 : 1) << 6);
+    }
     quad_of[o] = (int)H.quads.size();
     H.quads.push_back(q);
     return quad_of[o];
