@@ -349,27 +349,34 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
   // u,v (Sphere.cpp:136-140) are not computed: no texture kind reads them.
 }
 
-// Axis-aligned quads (DQuad::aa >= 0): with n, w on axis k and u, v on axes i, j,
-// every other term of Plane::hit's dot and cross products is a product with an
-// exact zero.  For a finite ray those terms are +-0 and vanish from the sums
-// exactly (a + +-0 == a for a != 0; a zero result only flips its sign, which no
-// test below reads), so
+// Axis-aligned quads (DQuad::aa >= 0; make_box faces, the Cornell walls): with
+// n, w on axis k and u, v on axes i, j, every other term of Plane::hit's dot and
+// cross products is a product with an exact zero, so
 //   denom = n_k d_k,  t = (D - n_k o_k) / denom,
-//   alpha = w_k (+-(pv_i v_j)),  beta = w_k (+-(u_i pv_j))   (sign: the parity of (k, i, j))
-// are the same doubles as the full formulas, at a third of the operations.  The
-// caller passes `fin` (ray origin and direction finite); a non-finite ray takes
-// the full formulas, whose NaN propagation it needs.
+//   alpha = w_k (+-(pv_i v_j)),  beta = w_k (+-(u_i pv_j))   (sign: parity of (k, i, j))
+// at a third of the operations, with the same outcome for EVERY ray:
+//  * finite ray: the dropped terms are +-0 and vanish from the sums exactly
+//    (a + +-0 == a for a != 0; a zero result may flip sign, which no test
+//    reads: 0 <= -0, and a zero t fails t >= tmin / enters the medium span as
+//    the same value);
+//  * non-finite ray: both forms reject.  The full form turns 0 * inf into a
+//    NaN dot product; this form rejects an infinite denominator explicitly
+//    (t would be 0) and otherwise accepts only with d_k, o_k (finite t) and
+//    o_i, d_i, o_j, d_j (finite alpha, beta) finite -- every component.
+// The quad's own values are finite (checked when aa is set).
 #ifndef RT_QUAD_AA
 #define RT_QUAD_AA 1
 #endif
+RT_HD RT_FI double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); } // no private array
 RT_HD RT_FI bool quad_t_aa(const DQuad &q, const Ray &r, double tmin, double tmax, double &t) {
   const int k = q.aa & 3, i = (q.aa >> 2) & 3, j = (q.aa >> 4) & 3;
-  const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-  const double denom = q.n[k] * d[k];
-  if (fabs(denom) < 1e-8) return false;
-  const double tt = (q.D - q.n[k] * o[k]) / denom;
+  const double denom = q.n[k] * comp(r.d, k);
+  // |denom| = inf: the full form's denom is NaN (0 * inf in the dot product)
+  if (fabs(denom) < 1e-8 || fabs(denom) == kInf) return false;
+  const double tt = (q.D - q.n[k] * comp(r.o, k)) / denom;
   if (!(tmin <= tt && tt <= tmax)) return false;
-  const double pvi = (o[i] + tt * d[i]) - q.Q[i], pvj = (o[j] + tt * d[j]) - q.Q[j];
+  const double pvi = (comp(r.o, i) + tt * comp(r.d, i)) - q.Q[i];
+  const double pvj = (comp(r.o, j) + tt * comp(r.d, j)) - q.Q[j];
   const double ca = pvi * q.v[j], cb = q.u[i] * pvj;
   const bool neg = (q.aa >> 6) & 1;
   const double alpha = q.w[k] * (neg ? -ca : ca);
@@ -378,14 +385,9 @@ RT_HD RT_FI bool quad_t_aa(const DQuad &q, const Ray &r, double tmin, double tma
   t = tt;
   return true;
 }
-RT_HD RT_FI bool ray_finite(const Ray &r) {
-  return isfinite(r.o.x) && isfinite(r.o.y) && isfinite(r.o.z) && isfinite(r.d.x) &&
-         isfinite(r.d.y) && isfinite(r.d.z);
-}
-
 RT_HD RT_FI bool quad_t(const DQuad &q, const Ray &r, double tmin, double tmax,
-                                       double &t, bool fin = false) { // Plane.cpp:76-100
-  if (RT_QUAD_AA && fin && q.aa >= 0) return quad_t_aa(q, r, tmin, tmax, t);
+                                       double &t) { // Plane.cpp:76-100
+  if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa(q, r, tmin, tmax, t);
   V3 n = ld3(q.n);
   double denom = dot(n, r.d);
   if (fabs(denom) < 1e-8) return false;
@@ -491,13 +493,11 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
     }
   };
   Ray lr = r;
-  bool lr_fin = ray_finite(r);
   int lr_first = -1, lr_count = 0; // chain lr is in (boundary items often share one)
   for (int k = 0; k < M.b_count; ++k) {
     const DItem it = S.bitems[M.b_first + k];
     if (it.xf_first != lr_first || it.xf_count != lr_count) {
       lr = it.xf_count ? to_local(S, it.xf_first, it.xf_count, r) : r;
-      lr_fin = ray_finite(lr);
       lr_first = it.xf_first;
       lr_count = it.xf_count;
     }
@@ -518,7 +518,7 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
     } else { // quad_t without its interval test
       const DQuad &q = S.quads[it.idx];
       double tt;
-      if (RT_QUAD_AA && lr_fin && q.aa >= 0) {
+      if (RT_QUAD_AA && q.aa >= 0) {
         if (!quad_t_aa(q, lr, -kInf, kInf, tt)) continue;
       } else {
         V3 n = ld3(q.n);
@@ -820,20 +820,17 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     tmin32 = f32_dn(tmin);
   }
   // closest-hit test of one world item (records only t and the item index)
-  const bool fin = ray_finite(r); // axis-aligned quad formulas (quad_t_aa) need it
   auto test_item = [&](int ii) {
     if (STATS) cnt.wleaf += wave_once();
     const DItem it = S.items[ii];
     Ray lr = r;
     double al = a;
     const double *pya = &ya;
-    bool lfin = fin;
     if constexpr ((F & F_XFORM) != 0) {
       if (it.xf_count) {
         lr = to_local(S, it.xf_first, it.xf_count, r);
         al = len2(lr.d);
         pya = nullptr; // a local ray has its own |d|^2: plain division
-        lfin = ray_finite(lr);
       }
     }
     double t;
@@ -843,7 +840,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t, moving, pya);
     } else {
       if (STATS) cnt.quads++;
-      hit = quad_t(S.quads[it.idx], lr, tmin, closest, t, lfin);
+      hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
     }
     if (hit) {
       closest = t;
@@ -954,7 +951,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
       if (STATS) cnt.light++;
       const DQuad &q = S.quads[L.idx];
       double t;
-      if (quad_t(q, lr, 0.001, kInf, t, ray_finite(lr))) {
+      if (quad_t(q, lr, 0.001, kInf, t)) {
         V3 n = ld3(q.n);
         V3 fn = dot(lr.d, n) < 0 ? n : -n;
         double d2 = t * t * len2(lr.d);

@@ -156,3 +156,34 @@ extern "C" void emu_slab(const double *o, const double *d, const float *lo, cons
     out[k] = v;
   }
 }
+
+// The axis-aligned quad formulas against the full Plane::hit formulas
+// (tests/test_emulator.py): the world's quads of `desc` (compiled by the
+// library's scene compiler, which sets DQuad::aa) against n rays (o, d: 3
+// doubles each) on [tmin, tmax]; out[4k..4k+3] = (hit, t) of quad_t on the quad
+// as compiled and (hit, t) with aa cleared, for quad k % n_quads.
+extern "C" int emu_quad_forms(const rt_scene_desc *desc, const double *o, const double *d,
+                              double tmin, double tmax, int n, double *out, int *n_aa) {
+  rtx::HostScene H;
+  std::string err;
+  if (rtx::compile_scene(desc, H, err) != RT_OK || H.quads.empty()) return -1;
+  *n_aa = 0;
+  for (const DQuad &q : H.quads) *n_aa += q.aa >= 0;
+  for (int k = 0; k < n; ++k) {
+    const DQuad &q = H.quads[k % H.quads.size()];
+    DQuad g = q;
+    g.aa = -1;
+    rtp::Ray r;
+    r.o = rtp::v3(o[3 * k], o[3 * k + 1], o[3 * k + 2]);
+    r.d = rtp::v3(d[3 * k], d[3 * k + 1], d[3 * k + 2]);
+    r.tm = 0.0;
+    double t0 = 0, t1 = 0;
+    const bool h0 = rtp::quad_t(q, r, tmin, tmax, t0);
+    const bool h1 = rtp::quad_t(g, r, tmin, tmax, t1);
+    out[4 * k] = h0;
+    out[4 * k + 1] = h0 ? t0 : 0.0;
+    out[4 * k + 2] = h1;
+    out[4 * k + 3] = h1 ? t1 : 0.0;
+  }
+  return 0;
+}
