@@ -66,6 +66,52 @@ class ProgressiveRenderer:
         self.samples_taken = 0
 
 
+class AdaptiveFrames:
+    """DynamicCamera's frame-rate controller (DynamicCamera.cpp:181-195) on this
+    renderer's per-frame knob.  The reference measures frames per second once a
+    second and doubles its tile size (16 -> 64, DynamicCamera.hpp:32-34) when
+    fps > 30, halves it when fps < 15, and stops adapting once converged.  Its
+    tile size only changes how a frame's work is scheduled; here a frame is one
+    launch, and the knob that trades frame rate for progress is the number of
+    strata traced per frame: doubled above 30 fps, halved below 15, within
+    [min_strata, max_strata] (default 1..4, the reference's 16..64 ratio).  The
+    converged image does not depend on it (every stratum is traced once).
+
+        ctl = AdaptiveFrames(pr)
+        while not pr.converged:
+            ctl.frame()          # traces ctl.strata strata, adapts once a second
+    """
+
+    def __init__(self, pr, min_strata=1, max_strata=4, clock=None, window_s=1.0):
+        import time
+        self.pr = pr
+        self.min_strata, self.max_strata = int(min_strata), int(max_strata)
+        self.strata = self.min_strata
+        self.clock = clock or time.perf_counter
+        self.window_s = window_s
+        self.fps = 0.0
+        self._frames = 0
+        self._t0 = self.clock()
+
+    def frame(self):
+        """One displayed frame: trace `strata` strata (0 once converged), then
+        update the frame-rate estimate and adapt (DynamicCamera.cpp:181-195)."""
+        n = self.pr.step(self.strata)
+        self._frames += 1
+        now = self.clock()
+        elapsed = now - self._t0
+        if elapsed >= self.window_s:
+            self.fps = self._frames / elapsed
+            self._frames = 0
+            self._t0 = now
+            converged = self.pr.converged
+            if not converged and self.fps > 30.0 and self.strata < self.max_strata:
+                self.strata = min(self.strata * 2, self.max_strata)
+            elif not converged and self.fps < 15.0 and self.strata > self.min_strata:
+                self.strata = max(self.strata // 2, self.min_strata)
+        return n
+
+
 def for_renderer(renderer, frame, seed=0, device=None, stream=None):
     """A ProgressiveRenderer over librtx_hip on a torch CUDA device."""
     import torch

@@ -91,3 +91,49 @@ def test_progressive_reset_on_camera_move():
         got = pr.acc.cpu().numpy()
     want = O.oracle_render(S, cam2, O.MODE_COUNTER, 2, output=abi.RT_OUT_SUM)
     np.testing.assert_allclose(got, want, rtol=0, atol=1e-4 * 4)
+
+
+def test_adaptive_frames_follow_the_reference_thresholds():
+    """AdaptiveFrames (DynamicCamera.cpp:181-195): once per 1 s window, > 30 fps
+    doubles the strata per frame up to the bound, < 15 fps halves it, 15..30
+    keeps it, and a converged renderer stops adapting; the converged
+    accumulation is the static render's sample sum whatever the schedule."""
+    from rtx.progressive import AdaptiveFrames
+    S = load_scene(SCENE)
+    cam = S.camera_desc(image_width=8, samples_per_pixel=256, max_depth=4)  # 16x16 strata
+    f = camera_frame(cam)
+    acc = torch.zeros((f.image_height, f.image_width, 3), dtype=torch.float64)
+    pr = ProgressiveRenderer(_oracle_fn(S, cam), f, acc, seed=3)
+    t = [0.0]
+    ctl = AdaptiveFrames(pr, min_strata=1, max_strata=4, clock=lambda: t[0])
+    seen = []
+
+    def run(frames, dt):
+        for _ in range(frames):
+            t[0] += dt
+            ctl.frame()
+            seen.append(ctl.strata)
+    run(130, 0.02)                     # 50 fps: 1 -> 2 -> 4 (bounded), one step a second
+    assert ctl.strata == 4 and seen[49] == 2 and seen[99] == 4 and seen[48] == 1
+    assert pr.converged                # 50 x 1 + 50 x 2 + 27 x 4 >= 256 strata
+    s_before = ctl.strata
+    run(30, 0.1)                       # 10 fps, but converged: no change
+    assert ctl.strata == s_before
+    full = O.oracle_render(S, cam, O.MODE_COUNTER, 3, output=abi.RT_OUT_SUM)
+    np.testing.assert_allclose(acc.numpy(), full, rtol=1e-12, atol=1e-12)
+    # not converged: slow frames halve, mid-band frames keep
+    acc2 = torch.zeros_like(acc)
+    pr2 = ProgressiveRenderer(lambda *a: None, f, acc2, seed=3)
+    t[0] = 0.0
+    ctl2 = AdaptiveFrames(pr2, min_strata=1, max_strata=4, clock=lambda: t[0])
+    ctl2.strata = 4
+    for _ in range(25):
+        t[0] += 0.1
+        ctl2.frame()                   # 10 fps: 4 -> 2 -> 1 over two windows
+    assert ctl2.strata == 1
+    pr2.samples_taken = 0
+    ctl2.strata = 2
+    for _ in range(25):
+        t[0] += 1 / 20.0
+        ctl2.frame()                   # 20 fps: inside the band
+    assert ctl2.strata == 2
