@@ -163,6 +163,9 @@ typedef struct rt_scene_desc {
   int32_t bvh_builder; /* RT_BVH_AUTO (0): device binned SAH from 65536 world
                           primitives, host SAH below; RT_BVH_HOST; RT_BVH_DEVICE
                           (linear BVH); RT_BVH_DEVICE_SAH */
+  int32_t bvh_arity;   /* world BVH node width: 0 = auto (4 from 16384 world
+                          primitives, else 2), 2, or 4 (the binary tree collapsed
+                          to 4-wide nodes) */
 } rt_scene_desc;
 
 enum {
@@ -277,11 +280,12 @@ typedef struct rt_scene_info {
   int32_t sphere_bytes; /* bytes per sphere record */
   int32_t quad_bytes;   /* bytes per quad record */
   int64_t device_bytes; /* total device bytes of the scene */
-  int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise */
+  int32_t features;     /* kernel instance: bit0 media, bit1 transforms, bit2 lights, bit3 noise,
+                           bit4 flat world, bit5 4-wide BVH */
   int32_t lds_nodes;    /* BVH nodes (BFS prefix) the kernel stages in LDS per block */
   int32_t bvh_builder;  /* the builder that made the world BVH: RT_BVH_HOST / RT_BVH_DEVICE /
                            RT_BVH_DEVICE_SAH */
-  int32_t _pad;
+  int32_t bvh_arity;    /* 2 or 4 (n_nodes, lds_nodes and node_bytes count nodes of this width) */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

@@ -57,6 +57,7 @@ struct rt_scene {
   double *scratch = nullptr; // chunk partials of chunked frame launches
   size_t scratch_bytes = 0;
   int wave_slots = 0;        // resident waves of the render instance on this device
+  double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
 };
 
 namespace {
@@ -263,12 +264,21 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   };
   std::vector<Part> parts;
   size_t off = 0;
-  auto add = [&](const void *src, size_t bytes) {
+  auto add = [&](const void *src, size_t bytes, size_t reserve = 0) {
     parts.push_back(Part{src, bytes, off});
-    off += align256(bytes ? bytes : 1);
+    reserve = std::max(reserve, bytes);
+    off += align256(reserve ? reserve : 1);
     return parts.size() - 1;
   };
-  size_t iN = add(H.nodes.data(), H.nodes.size() * sizeof(DNode));
+  // 4-wide world BVH (RT_FEAT_BVH4): asked for, or automatic from kBvh4Min
+  // primitives; collapsed from the binary tree once that exists (host or device
+  // build) into the node range, which is sized for it (<= one 4-wide node per
+  // binary node)
+  const int arity_req = desc->bvh_arity;
+  const bool want4 = arity_req == 4 || (arity_req == 0 && H.items.size() >= (size_t)rtx::kBvh4Min);
+  size_t iN = add(H.device_bvh ? nullptr : H.nodes.data(),
+                  H.device_bvh ? 0 : H.nodes.size() * sizeof(DNode),
+                  H.nodes.size() * (want4 ? sizeof(DNode4) : sizeof(DNode)));
   size_t iI = add(H.items.data(), H.items.size() * sizeof(DItem));
   size_t iB = add(H.bitems.data(), H.bitems.size() * sizeof(DItem));
   size_t iMI = add(H.mitems.data(), H.mitems.size() * sizeof(DItem));
@@ -307,6 +317,21 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     return hip_err(e, "stream/event create");
   }
   auto P = [&](size_t i) { return (const void *)(s->block + parts[i].off); };
+  // with H.nodes holding the final binary tree: collapse and upload the 4-wide
+  // one (kept binary when its stack would not fit RT_STACK_DEPTH4)
+  auto collapse4 = [&]() -> hipError_t {
+    if (!want4 || H.root_is_leaf || H.nodes.empty()) return hipSuccess;
+    const int d4 = rtx::collapse_bvh4(H.nodes, H.nodes4);
+    if (rtx::bvh4_stack_depth(d4) > RT_STACK_DEPTH4) {
+      H.nodes4.clear();
+      return hipSuccess;
+    }
+    s->binary_cost = rtx::bvh_sah_cost(H.nodes);
+    H.bvh_arity = 4;
+    H.bvh_depth4 = d4;
+    return hipMemcpy((void *)P(iN), H.nodes4.data(), H.nodes4.size() * sizeof(DNode4),
+                     hipMemcpyHostToDevice);
+  };
   DScene &d = s->ds;
   d.nodes = (const DNode *)P(iN);
   d.items = (const DItem *)P(iI);
@@ -358,6 +383,14 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       H.root_is_leaf = tree.root_leaf > 0;
       H.n_root_items = tree.root_leaf;
       builder = H.device_bvh;
+      if (want4 && !H.root_is_leaf) { // the collapse runs on the host copy
+        hipError_t ce = hipMemcpy(H.nodes.data(), P(iN), H.nodes.size() * sizeof(DNode),
+                                  hipMemcpyDeviceToHost);
+        if (ce != hipSuccess) {
+          rt_scene_destroy(s);
+          return hip_err(ce, "BVH download");
+        }
+      }
     } else { // too deep for the per-lane stack: rebuild on the host (depth-capped SAH)
       rtx::build_world_bvh_host(H);
       hipError_t ue = hipMemcpy((void *)P(iN), H.nodes.data(), H.nodes.size() * sizeof(DNode),
@@ -374,11 +407,21 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     d.root_is_leaf = H.root_is_leaf;
     d.n_root_items = H.n_root_items;
   }
+  if ((e = collapse4()) != hipSuccess) {
+    rt_scene_destroy(s);
+    return hip_err(e, "4-wide BVH upload");
+  }
   if (d.root_is_leaf) d.features |= RT_FEAT_FLAT;
   // traversal stack: one entry per BVH level suffices (a pushed entry is the
-  // sibling of a node on the current root path); LDS prefix of the BFS-ordered
-  // nodes sized to what the instance's occupancy leaves free
+  // sibling of a node on the current root path; three per level for 4-wide
+  // nodes); LDS prefix of the BFS-ordered nodes sized to what the instance's
+  // occupancy leaves free
   d.stack_depth = std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
+  if (H.bvh_arity == 4) {
+    d.features |= RT_FEAT_BVH4;
+    d.n_nodes = (int32_t)H.nodes4.size();
+    d.stack_depth = rtx::bvh4_stack_depth(H.bvh_depth4);
+  }
   {
     int budget = 0, wps = 1, cus = 0;
     hipError_t be = rtk_node_budget(d.features, d.stack_depth, &budget, &wps);
@@ -389,26 +432,27 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
     }
     if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
-    d.n_lds_nodes = std::max(0, std::min(budget, (int32_t)H.nodes.size()));
+    d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
   }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
 
   rt_scene_info &in = s->info;
   std::memset(&in, 0, sizeof in);
-  in.n_nodes = (int32_t)H.nodes.size();
+  in.n_nodes = d.n_nodes;
   in.n_leaf_refs = (int32_t)H.items.size(); // leaves are item ranges
   in.n_spheres = (int32_t)H.spheres.size();
   in.n_quads = (int32_t)H.quads.size();
   in.n_objects = (int32_t)(H.items.size() + H.mitems.size());
   in.n_light_leaves = (int32_t)H.lights.size();
   in.bvh_depth = H.bvh_depth;
-  in.node_bytes = (int32_t)sizeof(DNode);
+  in.node_bytes = (int32_t)(H.bvh_arity == 4 ? sizeof(DNode4) : sizeof(DNode));
   in.sphere_bytes = (int32_t)sizeof(DSphere);
   in.quad_bytes = (int32_t)sizeof(DQuad);
   in.device_bytes = (int64_t)off;
   in.features = d.features;
   in.lds_nodes = d.n_lds_nodes;
   in.bvh_builder = builder;
+  in.bvh_arity = H.bvh_arity;
   *out = s;
   return RT_OK;
 }
@@ -573,31 +617,17 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
 int rt_scene_bvh_cost(const rt_scene *s, double *cost) {
   if (!s || !cost) return set_err(RT_ERR_INVALID, "null argument");
   *cost = 0.0;
+  if (s->binary_cost >= 0.0) { // the device holds the 4-wide collapse
+    *cost = s->binary_cost;
+    return RT_OK;
+  }
   const int n = s->ds.n_nodes;
   if (s->ds.root_is_leaf || n <= 0) return RT_OK;
   std::vector<DNode> nodes(n);
   DeviceGuard g(s->device);
   hipError_t e = hipMemcpy(nodes.data(), s->ds.nodes, sizeof(DNode) * n, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_err(e, "hipMemcpy nodes");
-  auto area = [](const float *lo, const float *hi) {
-    const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
-    return 2.0 * (x * y + y * z + z * x);
-  };
-  float rlo[3], rhi[3];
-  for (int a = 0; a < 3; ++a) {
-    rlo[a] = std::min(nodes[0].lo0[a], nodes[0].lo1[a]);
-    rhi[a] = std::max(nodes[0].hi0[a], nodes[0].hi1[a]);
-  }
-  const double root = area(rlo, rhi);
-  if (!(root > 0.0)) return RT_OK;
-  double c = 1.0;
-  for (const DNode &d : nodes)
-    for (int k = 0; k < 2; ++k) {
-      const int e = d.entry[k];
-      const double w = e >= 0 ? 1.0 : (double)((~e) & 7);
-      c += w * area(k ? d.lo1 : d.lo0, k ? d.hi1 : d.hi0) / root;
-    }
-  *cost = c;
+  *cost = rtx::bvh_sah_cost(nodes);
   return RT_OK;
 }
 

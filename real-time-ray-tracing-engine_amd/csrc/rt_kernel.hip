@@ -42,7 +42,7 @@ using namespace rtp;
 #ifndef RT_REGEN_FLAT
 #define RT_REGEN_FLAT 16
 #endif
-#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : ((F) == 0 ? 16 : 1))
+#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? 16 : 1))
 #endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
@@ -61,7 +61,7 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 4
 #endif
-#define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : ((F) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
+#define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 
 template <bool STATS, unsigned F>
 __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
@@ -75,11 +75,12 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   const int wv = threadIdx.x >> 6;
   int *stack_base = reinterpret_cast<int *>(dyn_lds);
   DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + kWaves * S.stack_depth * 64);
-  const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g;
+  const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g; // DNode4 in BVH4 instances
+  constexpr int kNodeBytes = (F & F_BVH4) ? (int)sizeof(DNode4) : (int)sizeof(DNode);
   if (S.n_lds_nodes > 0) { // stage the top of the BVH (BFS prefix) once per block
     const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
     int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
-    const int n16 = S.n_lds_nodes * (int)(sizeof(DNode) / 16);
+    const int n16 = S.n_lds_nodes * (kNodeBytes / 16);
     for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
   }
@@ -221,9 +222,12 @@ __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint
 
 using RenderFn = void (*)(DScene, DCamera, DLaunch, double *, unsigned long long *);
 
+// F_BVH4 never comes with F_FLAT (a flat world has no tree): those slots reuse
+// the flat instance instead of instantiating a kernel that cannot be launched
+constexpr unsigned canonical(unsigned f) { return (f & F_FLAT) ? (f & ~F_BVH4) : f; }
 template <bool STATS, unsigned... Fs>
 constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequence<unsigned, Fs...>) {
-  return {render_tiles<STATS, Fs>...};
+  return {render_tiles<STATS, canonical(Fs)>...};
 }
 
 // one instance per feature set (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE | F_FLAT)
@@ -236,8 +240,9 @@ const RenderFn *render_table(bool stats) {
 } // namespace
 
 // ---------------------------------------------------------------- launchers
-extern "C" size_t rtk_lds_bytes(int stack_depth, int n_lds_nodes) {
-  return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * sizeof(DNode);
+extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) {
+  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
 
 // LDS bytes per block left for the staged BVH prefix at the occupancy the
@@ -256,8 +261,9 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
   const int blocks_per_cu = waves_per_simd * 4 / kWaves > 0 ? waves_per_simd * 4 / kWaves : 1;
   size_t per_block = lds_cu / blocks_per_cu;
   if (per_block > cap) per_block = cap;
-  size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(stack_depth, 0);
-  *n_nodes = per_block > fixed ? (int)((per_block - fixed) / sizeof(DNode)) : 0;
+  size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(features, stack_depth, 0);
+  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  *n_nodes = per_block > fixed ? (int)((per_block - fixed) / node) : 0;
   return hipSuccess;
 }
 
@@ -267,7 +273,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   int blocks = (P->n_local_tiles * P->n_chunks + kWaves - 1) / kWaves;
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
-  size_t lds = rtk_lds_bytes(S->stack_depth, S->n_lds_nodes);
+  size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, *P, out, stats);
   return hipGetLastError();
 }

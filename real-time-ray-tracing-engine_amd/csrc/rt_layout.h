@@ -28,6 +28,7 @@
 #define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
 #define RT_N_STATS 18      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
+#define RT_STACK_DEPTH4 64 // 4-wide walks push up to three entries per level
 #ifndef RT_FLAT_MAX
 #define RT_FLAT_MAX 8 // worlds of at most this many items are one flat leaf (no BVH walk)
 #endif
@@ -89,6 +90,17 @@ struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + li
                      // items [first, first + count) (items are stored in leaf order)
   int32_t pad[2];
 };
+
+// 4-wide BVH node (128 B): the boxes of up to four children in SoA order
+// (lo x[4], lo y[4], lo z[4], hi x[4], ...), fp32 rounded outward like DNode's,
+// and their entries with DNode's encoding (-1 = empty slot).  Collapsed from the
+// binary tree for large scenes (rt_scene.cpp collapse_bvh4; RT_FEAT_BVH4).
+struct DNode4 {
+  float lo[3][4], hi[3][4];
+  int32_t entry[4];
+  int32_t pad[4];
+};
+static_assert(sizeof(DNode4) == 128, "DNode4 layout");
 
 struct DMat {        // 48 B
   int32_t kind, tex;
@@ -160,6 +172,7 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_LIGHTS 4 // non-empty light list
 #define RT_FEAT_NOISE 8  // Perlin noise textures
 #define RT_FEAT_FLAT 16  // flat world (root_is_leaf): no BVH walk
+#define RT_FEAT_BVH4 32  // the world BVH is 4-wide (DNode4); never with RT_FEAT_FLAT
 
 struct DCamera {     // the rt_frame values the kernel needs
   double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];

@@ -221,7 +221,8 @@ enum : unsigned {
   F_LIGHTS = 4u, // a non-empty light list (mixture with light sampling)
   F_NOISE = 8u,  // Perlin noise textures
   F_FLAT = 16u,  // flat world (root_is_leaf): every item tested in list order, no BVH walk
-  F_ALL = 31u
+  F_BVH4 = 32u,  // 4-wide world BVH (DNode4); never with F_FLAT
+  F_ALL = 63u
 };
 
 // ---------------------------------------------------------------- textures
@@ -872,6 +873,65 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       cur = 0;
     }
     for (;;) {
+      if constexpr ((F & F_BVH4) != 0) {
+        // 4-wide node: four slab tests, the hits sorted near to far by a
+        // 5-comparator network, the far ones pushed (farthest first), the
+        // nearest walked next -- the binary walk's near-first order per level
+        const RT_LDS DNode4 *lnodes4 = (const RT_LDS DNode4 *)lnodes;
+        const DNode4 *nodes4 = (const DNode4 *)S.nodes;
+        while (cur >= 0) {
+          if (STATS) cnt.wnode += wave_once();
+          if (wave_none(ln == 0)) break;
+          if (STATS) cnt.nodes++;
+          DNode4 N;
+          if (cur < S.n_lds_nodes) {
+            const RT_LDS DNode4 &L = lnodes4[cur];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                N.lo[a][c] = L.lo[a][c];
+                N.hi[a][c] = L.hi[a][c];
+              }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) N.entry[c] = L.entry[c];
+          } else {
+            N = nodes4[cur];
+          }
+          float tn[4];
+          int en[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float lo[3] = {N.lo[0][c], N.lo[1][c], N.lo[2][c]};
+            const float hi[3] = {N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+            en[c] = N.entry[c];
+            tn[c] = en[c] == -1 ? __builtin_huge_valf() : slab(q, lo, hi, tmin32, cl32);
+          }
+          auto cswap = [&](int x, int y) {
+            const bool sw = tn[y] < tn[x];
+            const float tx = tn[x], ty = tn[y];
+            const int ex = en[x], ey = en[y];
+            tn[x] = sw ? ty : tx;
+            tn[y] = sw ? tx : ty;
+            en[x] = sw ? ey : ex;
+            en[y] = sw ? ex : ey;
+          };
+          cswap(0, 1);
+          cswap(2, 3);
+          cswap(0, 2);
+          cswap(1, 3);
+          cswap(1, 2);
+#pragma unroll
+          for (int c = 3; c >= 1; --c)
+            if (tn[c] != __builtin_huge_valf() && sp < S.stack_depth) stk[64 * sp++] = en[c];
+          cur = tn[0] != __builtin_huge_valf() ? en[0] : (sp > 0 ? stk[64 * --sp] : -1);
+          if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
+            lf = (~cur) >> 3;
+            ln = (~cur) & 7;
+            cur = sp > 0 ? stk[64 * --sp] : -1;
+          }
+        }
+      } else
       while (cur >= 0) {
         if (STATS) cnt.wnode += wave_once();
         if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them

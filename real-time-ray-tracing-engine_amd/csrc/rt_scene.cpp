@@ -951,7 +951,101 @@ void build_world_bvh_host(HostScene &H) {
   SahBuilder(H).emit_world_bvh(boxes);
 }
 
+double bvh_sah_cost(const std::vector<DNode> &nodes) {
+  if (nodes.empty()) return 0.0;
+  auto area = [](const float *lo, const float *hi) {
+    const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+    return 2.0 * (x * y + y * z + z * x);
+  };
+  float rlo[3], rhi[3];
+  for (int a = 0; a < 3; ++a) {
+    rlo[a] = std::min(nodes[0].lo0[a], nodes[0].lo1[a]);
+    rhi[a] = std::max(nodes[0].hi0[a], nodes[0].hi1[a]);
+  }
+  const double root = area(rlo, rhi);
+  if (!(root > 0.0)) return 0.0;
+  double c = 1.0;
+  for (const DNode &d : nodes)
+    for (int k = 0; k < 2; ++k) {
+      const int e = d.entry[k];
+      const double w = e >= 0 ? 1.0 : (double)((~e) & 7);
+      c += w * area(k ? d.lo1 : d.lo0, k ? d.hi1 : d.hi0) / root;
+    }
+  return c;
+}
+
+int collapse_bvh4(const std::vector<DNode> &bin, std::vector<DNode4> &out) {
+  out.clear();
+  if (bin.empty()) return 0;
+  struct Child {
+    float lo[3], hi[3];
+    int32_t e;
+  };
+  auto child = [&](const DNode &b, int k) {
+    Child c;
+    for (int a = 0; a < 3; ++a) {
+      c.lo[a] = k ? b.lo1[a] : b.lo0[a];
+      c.hi[a] = k ? b.hi1[a] : b.hi0[a];
+    }
+    c.e = b.entry[k];
+    return c;
+  };
+  auto area = [](const Child &c) {
+    const double x = (double)c.hi[0] - c.lo[0], y = (double)c.hi[1] - c.lo[1],
+                 z = (double)c.hi[2] - c.lo[2];
+    return x * y + y * z + z * x;
+  };
+  std::vector<int> src{0}, level{1}; // binary root and level of each 4-wide node
+  int depth = 0;
+  for (size_t k = 0; k < src.size(); ++k) {
+    const DNode &b = bin[src[k]];
+    Child c[4];
+    int n = 2;
+    c[0] = child(b, 0);
+    c[1] = child(b, 1);
+    while (n < 4) {
+      int pick = -1;
+      double best = -1.0;
+      for (int i = 0; i < n; ++i)
+        if (c[i].e >= 0 && area(c[i]) > best) {
+          best = area(c[i]);
+          pick = i;
+        }
+      if (pick < 0) break;
+      const DNode &m = bin[c[pick].e];
+      for (int i = n; i > pick + 1; --i) c[i] = c[i - 1]; // keep the leaf order
+      c[pick] = child(m, 0);
+      c[pick + 1] = child(m, 1);
+      ++n;
+    }
+    DNode4 q;
+    std::memset(&q, 0, sizeof q);
+    for (int i = 0; i < 4; ++i) {
+      for (int a = 0; a < 3; ++a) {
+        q.lo[a][i] = i < n ? c[i].lo[a] : std::numeric_limits<float>::infinity();
+        q.hi[a][i] = i < n ? c[i].hi[a] : -std::numeric_limits<float>::infinity();
+      }
+      if (i >= n) {
+        q.entry[i] = -1;
+      } else if (c[i].e >= 0) {
+        q.entry[i] = (int32_t)src.size();
+        src.push_back(c[i].e);
+        level.push_back(level[k] + 1);
+      } else {
+        q.entry[i] = c[i].e;
+      }
+    }
+    depth = std::max(depth, level[k]);
+    out.push_back(q);
+  }
+  return depth;
+}
+
 int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err) {
+  if (desc && desc->bvh_arity != 0 && desc->bvh_arity != 2 && desc->bvh_arity != 4) {
+    err = "bvh_arity must be 0 (auto), 2 or 4";
+    return RT_ERR_INVALID;
+  }
   Compiler c(desc, out, err);
   if (!c.run()) return err.rfind("UNSUPPORTED", 0) == 0 ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID;
   return RT_OK;

@@ -11,6 +11,7 @@ namespace rtx {
 
 struct HostScene {
   std::vector<DNode> nodes;
+  std::vector<DNode4> nodes4; // the world BVH collapsed to 4-wide nodes (bvh_arity 4)
   std::vector<DItem> items;
   std::vector<DItem> mitems; // media (not in the BVH)
   std::vector<float> mbox;   // 6 per medium
@@ -26,6 +27,8 @@ struct HostScene {
   int32_t root_is_leaf = 0;
   int32_t n_root_items = 0;
   int32_t bvh_depth = 0;
+  int32_t bvh_arity = 2;  // 4: nodes4 is the tree the kernel walks
+  int32_t bvh_depth4 = 0; // levels of 4-wide nodes
   // device-built world BVH (0: built on the host; RT_BVH_DEVICE: linear BVH,
   // rt_bvh_build.hip; RT_BVH_DEVICE_SAH: binned SAH, rt_bvh_sah.hip): items still
   // in scene order, their boxes (lo xyz, hi xyz) and the centroid bounds; nodes
@@ -49,6 +52,26 @@ constexpr int kDeviceBuildMin = 65536;
 
 // Host SAH build from HostScene::item_boxes (fallback of the device build).
 void build_world_bvh_host(HostScene &H);
+
+// Scenes with at least this many world primitives walk a 4-wide BVH when
+// rt_scene_desc.bvh_arity is 0 (auto).
+constexpr int kBvh4Min = 16384;
+
+// Collapses the binary BFS-ordered tree `bin` (root 0) into 4-wide nodes, BFS
+// order, root 0: each 4-wide node starts from one binary node's two children
+// and repeatedly replaces its largest-area inner child by that child's two
+// children until it holds four (or only leaves).  Leaf entries keep their
+// encoding, so the leaf item ranges are shared with the binary tree.  Returns
+// the number of 4-wide levels.
+int collapse_bvh4(const std::vector<DNode> &bin, std::vector<DNode4> &out);
+
+// SAH cost of a binary tree (rt_scene_bvh_cost): 1 + sum over child boxes of
+// (1 for an inner child, its item count for a leaf) x area / root area.
+double bvh_sah_cost(const std::vector<DNode> &nodes);
+
+// The traversal stack a 4-wide walk of depth4 levels needs: at most three
+// pushed siblings per level on the current root path.
+inline int bvh4_stack_depth(int depth4) { return 3 * depth4 + 1; }
 
 // Returns RT_OK or an error code with `err` filled.
 int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err);

@@ -60,10 +60,12 @@ class SceneDesc(C.Structure):
                 ("n_objects", C.c_int32), ("objects", C.POINTER(ObjectDesc)),
                 ("children", C.POINTER(C.c_int32)), ("n_children", C.c_int32),
                 ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32),
-                ("bvh_builder", C.c_int32)]
+                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32)]
 
 
 RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
+# kernel instance bits (rt_scene_info.features)
+RT_FEAT_MEDIA, RT_FEAT_XFORM, RT_FEAT_LIGHTS, RT_FEAT_NOISE, RT_FEAT_FLAT, RT_FEAT_BVH4 = 1, 2, 4, 8, 16, 32
 
 
 class CameraDesc(C.Structure):
@@ -110,7 +112,7 @@ class SceneInfo(C.Structure):
                 ("bvh_depth", C.c_int32), ("node_bytes", C.c_int32),
                 ("sphere_bytes", C.c_int32), ("quad_bytes", C.c_int32),
                 ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32),
-                ("bvh_builder", C.c_int32), ("_pad", C.c_int32)]
+                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

@@ -94,6 +94,7 @@ class SceneDescription:
         self.lights = -1
         self.use_bvh = 0
         self.bvh_builder = abi.RT_BVH_AUTO
+        self.bvh_arity = 0  # 0 auto, 2 or 4
         self.camera = None
         self._named_tex = {}
         self._named_mat = {}
@@ -146,6 +147,7 @@ class SceneDescription:
         d.children, d.n_children = K, len(self.children)
         d.world, d.lights, d.use_bvh = self.world, self.lights, int(self.use_bvh)
         d.bvh_builder = int(self.bvh_builder)
+        d.bvh_arity = int(self.bvh_arity)
         return d
 
     def camera_desc(self, **overrides):

@@ -61,8 +61,13 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   std::string err;
   if (rtx::compile_scene(desc, H, err) != RT_OK) return -1;
   if (H.device_bvh) rtx::build_world_bvh_host(H); // the device builder needs a GPU
+  // features bit 5 (F_BVH4): walk the 4-wide collapse of the same tree, as the
+  // library does for large scenes (rt_api.cpp)
+  const bool bvh4 = (features & F_BVH4) && !H.root_is_leaf && !H.nodes.empty();
+  int depth4 = 0;
+  if (bvh4) depth4 = rtx::collapse_bvh4(H.nodes, H.nodes4);
   DScene S;
-  S.nodes = H.nodes.data();
+  S.nodes = bvh4 ? (const DNode *)(const void *)H.nodes4.data() : H.nodes.data();
   S.items = H.items.data();
   S.bitems = H.bitems.data();
   S.mitems = H.mitems.data();
@@ -77,13 +82,14 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   S.perlin = H.perlin.data();
   S.lights = H.lights.data();
   S.n_lights = (int32_t)H.lights.size();
-  S.n_nodes = (int32_t)H.nodes.size();
+  S.n_nodes = (int32_t)(bvh4 ? H.nodes4.size() : H.nodes.size());
   S.root_is_leaf = H.root_is_leaf;
   S.n_root_items = H.n_root_items;
   S.features = features;
   S.static_spheres = rtx::all_spheres_static(H);
-  S.stack_depth = std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
-  S.n_lds_nodes = (int32_t)H.nodes.size(); // host: the "LDS" copy is the array itself
+  S.stack_depth = bvh4 ? rtx::bvh4_stack_depth(depth4)
+                       : std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
+  S.n_lds_nodes = S.n_nodes; // host: the "LDS" copy is the array itself
   DCamera C;
   auto cp = [](double *d, const rt_vec3 &v) {
     d[0] = v.x;
@@ -108,10 +114,10 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   if (r0 == 0 && r1 == 0) r1 = f->image_height;
   int n = f->sqrt_spp * f->sqrt_spp;
   int s0 = p->sample_begin, s1 = p->sample_count < 0 ? n : s0 + p->sample_count;
-  std::vector<int> stack(RT_STACK_DEPTH * 64);
+  std::vector<int> stack(std::max(RT_STACK_DEPTH, RT_STACK_DEPTH4) * 64);
   // the instance the library would pick: the caller's feature bits plus F_FLAT
-  // for a flat world (rt_api.cpp)
-  PixelFn fn = kFns[(features & 15) | (H.root_is_leaf ? F_FLAT : 0u)];
+  // for a flat world, F_BVH4 for a collapsed tree (rt_api.cpp)
+  PixelFn fn = kFns[(features & 15) | (H.root_is_leaf ? F_FLAT : 0u) | (bvh4 ? F_BVH4 : 0u)];
   for (int j = r0; j < r1; ++j)
     for (int i = 0; i < C.W; ++i) {
       double acc[3] = {0, 0, 0};
@@ -122,6 +128,68 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
       o[1] = (p->output == RT_OUT_SCALED) ? sc * acc[1] : acc[1];
       o[2] = (p->output == RT_OUT_SCALED) ? sc * acc[2] : acc[2];
     }
+  return 0;
+}
+
+// The 4-wide collapse of the world BVH of `desc` (tests/test_emulator.py):
+// info = {binary nodes, 4-wide nodes, binary depth, 4-wide levels, leaf entries
+// of the binary tree, leaf entries of the 4-wide tree, 1 if the two leaf-entry
+// lists are equal in order, inner children with a box different from the binary
+// node they came from, empty slots, 1 if every inner entry points forward (BFS)}
+extern "C" int emu_bvh4_info(const rt_scene_desc *desc, long long *info) {
+  rtx::HostScene H;
+  std::string err;
+  if (rtx::compile_scene(desc, H, err) != RT_OK) return -1;
+  if (H.device_bvh) rtx::build_world_bvh_host(H);
+  if (H.root_is_leaf || H.nodes.empty()) return -2;
+  const int d4 = rtx::collapse_bvh4(H.nodes, H.nodes4);
+  // leaf entries in depth-first child order, both trees
+  std::vector<int> lb, l4;
+  std::vector<int> st{0};
+  auto walk2 = [&](auto &&self, int n) -> void {
+    for (int k = 0; k < 2; ++k) {
+      const int e = H.nodes[n].entry[k];
+      if (e >= 0) self(self, e);
+      else lb.push_back(e);
+    }
+  };
+  walk2(walk2, 0);
+  long long empty = 0, forward = 1;
+  auto walk4 = [&](auto &&self, int n) -> void {
+    for (int k = 0; k < 4; ++k) {
+      const int e = H.nodes4[n].entry[k];
+      if (e == -1) ++empty;
+      else if (e >= 0) {
+        if (e <= n) forward = 0;
+        self(self, e);
+      } else l4.push_back(e);
+    }
+  };
+  walk4(walk4, 0);
+  // every child box of a 4-wide node is a child box of some binary node
+  std::vector<std::array<float, 6>> bb;
+  for (const DNode &n : H.nodes) {
+    bb.push_back({n.lo0[0], n.lo0[1], n.lo0[2], n.hi0[0], n.hi0[1], n.hi0[2]});
+    bb.push_back({n.lo1[0], n.lo1[1], n.lo1[2], n.hi1[0], n.hi1[1], n.hi1[2]});
+  }
+  std::sort(bb.begin(), bb.end());
+  long long foreign = 0;
+  for (const DNode4 &q : H.nodes4)
+    for (int k = 0; k < 4; ++k)
+      if (q.entry[k] != -1) {
+        std::array<float, 6> b{q.lo[0][k], q.lo[1][k], q.lo[2][k], q.hi[0][k], q.hi[1][k], q.hi[2][k]};
+        foreign += !std::binary_search(bb.begin(), bb.end(), b);
+      }
+  info[0] = (long long)H.nodes.size();
+  info[1] = (long long)H.nodes4.size();
+  info[2] = H.bvh_depth;
+  info[3] = d4;
+  info[4] = (long long)lb.size();
+  info[5] = (long long)l4.size();
+  info[6] = lb == l4;
+  info[7] = foreign;
+  info[8] = empty;
+  info[9] = forward;
   return 0;
 }
 

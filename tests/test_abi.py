@@ -117,6 +117,12 @@ def test_scene_validation_errors_precede_device_use():
                                                 "radius": 1}}}]}
     rc, msg = _create(doc)
     assert rc == abi.RT_ERR_UNSUPPORTED and "medium" in msg
+    # BVH node width is 0 (auto), 2 or 4
+    S3 = load_scene(base)
+    S3.bvh_arity = 3
+    d3 = S3.desc()
+    assert L.rt_scene_create(C.byref(d3), 0, C.byref(h)) == abi.RT_ERR_INVALID
+    assert "bvh_arity" in L.rt_last_error().decode()
 
 
 def test_scene_json_errors():

@@ -1,0 +1,76 @@
+"""4-wide world BVH (RT_FEAT_BVH4; VERDICT r1 item 9: BVH arity per scene size).
+The binary tree (host or device built) is collapsed into 4-wide nodes
+(rt_scene.cpp collapse_bvh4) for scenes of at least kBvh4Min = 16384 world
+primitives, or when rt_scene_desc.bvh_arity asks for it.  The closest hit does
+not depend on the tree, so images equal the binary walk's (1e-12: an exact tie
+between two surfaces may resolve the other way round) and the oracle's."""
+import os
+
+import numpy as np
+import pytest
+
+from rtx import abi
+from rtx.render import Renderer, camera_frame
+from rtx.scene import load_scene
+import oracle_lib as O
+from test_device_bvh import random_spheres, compare
+
+pytestmark = pytest.mark.gpu
+SCENES = os.path.join(O.ROOT, "real-time-ray-tracing-engine_amd", "scenes")
+
+
+def render_arity(S, f, arity, seed):
+    S.bvh_arity = arity
+    with Renderer(S) as R:
+        info = R.info()
+        img = R.render(f, seed=seed)
+        cost = R.bvh_cost()
+    return info, img, cost
+
+
+@pytest.mark.parametrize("name,w,spp", [("bouncing_seed42", 48, 4), ("cornell_fog", 32, 9)])
+def test_forced_bvh4_matches_binary_and_oracle(name, w, spp):
+    S = load_scene(os.path.join(SCENES, name + ".json"))
+    cam = S.camera_desc(image_width=w, samples_per_pixel=spp, max_depth=8)
+    f = camera_frame(cam)
+    i2, a, c2 = render_arity(S, f, 2, 9)
+    i4, b, c4 = render_arity(S, f, 4, 9)
+    assert i2["bvh_arity"] == 2 and not i2["features"] & abi.RT_FEAT_BVH4
+    if i2["features"] & abi.RT_FEAT_FLAT:  # a flat world has no tree to collapse
+        assert i4["bvh_arity"] == 2
+    else:
+        assert i4["bvh_arity"] == 4 and i4["features"] & abi.RT_FEAT_BVH4
+        assert i4["node_bytes"] == 128 and i4["n_nodes"] <= i2["n_nodes"]
+        assert c4 == c2  # rt_scene_bvh_cost reports the binary tree either way
+    compare(b, a, 1e-12)
+    compare(b, O.oracle_render(S, cam, O.MODE_COUNTER, 9), 1e-4)
+
+
+def test_auto_arity_by_scene_size():
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    with Renderer(S) as R:
+        assert R.info()["bvh_arity"] == 2
+    S = load_scene(random_spheres(20000, seed=7))  # >= kBvh4Min, below the device-build size
+    cam = S.camera_desc(image_width=48, samples_per_pixel=4, max_depth=6)
+    f = camera_frame(cam)
+    i0, auto, _ = render_arity(S, f, 0, 3)
+    assert i0["bvh_arity"] == 4 and i0["bvh_builder"] == abi.RT_BVH_HOST
+    _, binary, _ = render_arity(S, f, 2, 3)
+    compare(auto, binary, 1e-12)
+    assert np.nanmean(auto) > 0
+
+
+@pytest.mark.parametrize("builder", [abi.RT_BVH_DEVICE_SAH, abi.RT_BVH_DEVICE])
+def test_bvh4_over_device_built_trees(builder):
+    """100k spheres: the device-built tree is copied back, collapsed and
+    re-uploaded; images equal the binary walk of the same tree."""
+    S = load_scene(random_spheres(100000, seed=3))
+    S.bvh_builder = builder
+    cam = S.camera_desc(image_width=64, samples_per_pixel=4, max_depth=6)
+    f = camera_frame(cam)
+    i4, b, c4 = render_arity(S, f, 0, 4)
+    i2, a, c2 = render_arity(S, f, 2, 4)
+    assert i4["bvh_arity"] == 4 and i4["bvh_builder"] == builder
+    assert i4["n_nodes"] < 0.6 * i2["n_nodes"]
+    assert c4 == c2
+    compare(b, a, 1e-12)

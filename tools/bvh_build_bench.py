@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """World-BVH build: host binned SAH vs device LBVH (rt_bvh_build.hip) vs device
-binned SAH (rt_bvh_sah.hip).
+binned SAH (rt_bvh_sah.hip), each walked as a binary or a 4-wide BVH.
 
 For N random spheres: rt_scene_create time (compile + upload + build) with each
 builder, the tree depth, and the render rate through each tree (1920x1080,
-spp 4, depth 8).   python tools/bvh_build_bench.py [--n 100000 500000]"""
+spp 4, depth 8).
+  python tools/bvh_build_bench.py [--n 100000 500000] [--arity 2 4] [--builders device_sah]"""
 import argparse
 import json
 import os
@@ -40,14 +41,19 @@ def scene(n, seed=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, nargs="+", default=[100000, 500000])
+    ap.add_argument("--arity", type=int, nargs="+", default=[2, 4])
+    ap.add_argument("--builders", nargs="+", default=["host_sah", "device_lbvh", "device_sah"])
     a = ap.parse_args()
+    by_name = {"host_sah": abi.RT_BVH_HOST, "device_lbvh": abi.RT_BVH_DEVICE,
+               "device_sah": abi.RT_BVH_DEVICE_SAH}
     for n in a.n:
         S = scene(n)
         cam = S.camera_desc(image_width=1920, samples_per_pixel=4, max_depth=8)
         f = camera_frame(cam)
         buf = torch.zeros((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda")
-        for b in (abi.RT_BVH_HOST, abi.RT_BVH_DEVICE, abi.RT_BVH_DEVICE_SAH):
+        for b, ar in [(by_name[x], ar) for x in a.builders for ar in a.arity]:
             S.bvh_builder = b
+            S.bvh_arity = ar
             S.desc()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -66,6 +72,7 @@ def main():
             name = {abi.RT_BVH_HOST: "host_sah", abi.RT_BVH_DEVICE: "device_lbvh",
                     abi.RT_BVH_DEVICE_SAH: "device_sah"}[b]
             print(json.dumps({"n": n, "builder": name, "built_by": info["bvh_builder"],
+                              "arity": info["bvh_arity"], "lds_nodes": info["lds_nodes"],
                               "create_s": round(t_create, 4), "bvh_depth": info["bvh_depth"],
                               "nodes": info["n_nodes"], "sah_cost": round(cost, 2),
                               "render_Msamples_s": round(f.image_width * f.image_height * 4 / min(ms) / 1e3, 1)}),
