@@ -326,6 +326,10 @@ def main():
     ap.add_argument("--n1-layout", default="frame", choices=["frame", "tiles"],
                     help="N=1: render straight into the frame (default) or in 8x8 tile "
                          "work units + chunk sum + tile->frame reorder, as the N>1 path")
+    ap.add_argument("--pg-rehearsal", action="store_true",
+                    help="N=1: still create the process group and run the N>1 exchange "
+                         "(RCCL gather/reduce over a world of one) -- exercises the "
+                         "collective path the driver's multi-GPU runs take on one GPU")
     ap.add_argument("--check", action="store_true",
                     help="rank 0 compares the reduced frame with a 1-device render")
     ap.add_argument("--pmc", default="auto", choices=["auto", "file", "off"],
@@ -349,7 +353,8 @@ def main():
         local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if ws > 1:
+    use_pg = ws > 1 or args.pg_rehearsal
+    if use_pg:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -367,7 +372,7 @@ def main():
     n_strata = sq * sq
     s0 = rank * n_strata // ws
     s1 = (rank + 1) * n_strata // ws
-    tiles_mode = (ws > 1 and args.shard == "tiles") or (ws == 1 and args.n1_layout == "tiles")
+    tiles_mode = (use_pg and args.shard == "tiles") or (ws == 1 and args.n1_layout == "tiles")
 
     from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks
     R = Renderer(scene, device=local)
@@ -407,13 +412,13 @@ def main():
         if rank == 0:
             if tiles_mode:
                 # reorder the gathered tiles (N=1: this rank's own tile sums)
-                final["frame"] = shard.frame_sums(gath[b] if ws > 1 else tsum[b].unsqueeze(0))
+                final["frame"] = shard.frame_sums(gath[b] if use_pg else tsum[b].unsqueeze(0))
             else:
                 final["frame"] = bufs[b]
             final["step"] = k
 
     def exchange(b):
-        if ws == 1:
+        if not use_pg:
             return None
         if tiles_mode:
             if args.backend == "nccl":
@@ -446,7 +451,7 @@ def main():
     drain()
     torch.cuda.synchronize(dev)
 
-    if ws > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -456,7 +461,7 @@ def main():
             kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
     drain()
     torch.cuda.synchronize(dev)
-    if ws > 1:
+    if use_pg:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     check = None
@@ -555,7 +560,7 @@ def main():
         "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
                    "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
                    "parallelism": (("1 GPU, tile work units x%d chunks" % shard.chunks
-                                    if tiles_mode else "1 GPU") if ws == 1 else
+                                    if tiles_mode else "1 GPU") if not use_pg else
                                    "tile-shard x%d (tile t on rank t %% %d, %d stratum chunks) + %s gather" % (
                                        ws, ws, shard.chunks,
                                        "RCCL" if args.backend == "nccl" else "gloo")
@@ -573,7 +578,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     R.close()
-    if ws > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

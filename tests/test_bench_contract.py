@@ -79,3 +79,25 @@ def test_bench_two_ranks_one_gpu(shard):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["check"]["ok"], d["check"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shard", ["tiles", "strata"])
+def test_bench_rccl_exchange_world_of_one(shard):
+    """The RCCL calls of the N>1 path (async gather of tile sums / async reduce of
+    stratum sums, .wait() before reuse of the double buffer) on a real
+    process group over RCCL -- a world of one, the most this one-GPU box can run
+    (RCCL refuses two ranks on one device); the frame must match a
+    single-device render (--check)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "C1", "--steps", "3",
+           "--warmup", "1", "--backend", "nccl", "--pg-rehearsal", "--check", "--shard", shard,
+           "--pmc", "off", "--no-cpu-baseline", "--no-other-configs"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert "RCCL" in d["config"]["parallelism"], d["config"]
+    assert d["check"]["ok"], d["check"]
