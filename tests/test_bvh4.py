@@ -74,3 +74,17 @@ def test_bvh4_over_device_built_trees(builder):
     assert i4["n_nodes"] < 0.6 * i2["n_nodes"]
     assert c4 == c2
     compare(b, a, 1e-12)
+
+
+@pytest.mark.parametrize("F", list(range(16)))
+def test_each_bvh4_instance_matches_oracle(F):
+    """Every non-flat feature set through its 4-wide instance (F | F_BVH4)."""
+    from test_gpu_instances import feature_scene
+    S = load_scene(feature_scene(F))
+    S.bvh_arity = 4
+    cam = S.camera_desc(image_width=32, samples_per_pixel=9, max_depth=8)
+    with Renderer(S) as R:
+        info = R.info()
+        assert info["features"] == F | abi.RT_FEAT_BVH4, info["features"]
+        img = R.render(camera_frame(cam), seed=21)
+    compare(img, O.oracle_render(S, cam, O.MODE_COUNTER, 21), 1e-4)
