@@ -226,6 +226,53 @@ enum : unsigned {
 };
 
 // ---------------------------------------------------------------- textures
+// sin(x) for NoiseTexture::value (NoiseTexture.cpp:33), within 1 ulp (checked
+// against long double in tests/test_emulator.py).  The library's double sin
+// carries a Payne-Hanek reduction for huge arguments whose temporaries are live
+// beside the whole path state at this point -- 16 of the rich instance's 28
+// spilled VGPRs.  Here: Cody-Waite reduction by pi/2 = P1 + P2 + P3 (P1 the
+// double nearest pi/2, so x - n P1 is exact for |x| < 2^20: both are multiples
+// of 2^-53 and the difference is below 1), the rest as a double-double
+// (TwoSum, exact product tail by FMA), then the fdlibm kernels (k_sin.c /
+// k_cos.c, Sun Microsystems 1993, freely redistributable) on |r| <= pi/4.
+// Larger or non-finite arguments go to the library sin out of line.
+#ifndef RT_SIN_N
+#define RT_SIN_N 1 // 0: the library sin (A/B builds)
+#endif
+RT_HD __attribute__((noinline)) double sin_wide(double x) { return sin(x); }
+RT_HD RT_FI double sin_n(double x) {
+  if (!(fabs(x) < 0x1p20)) return sin_wide(x);
+  const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54,
+               P3 = -0x1.f1976b7ed8fbcp-110;
+  const double n = rint(x * 0x1.45f306dc9c883p-1);
+  const double r1 = fma(-n, P1, x); // exact
+  const double p = n * P2, pe = fma(n, P2, -p);
+  const double hi = r1 - p, bb = hi - r1;
+  const double lo = ((r1 - (hi - bb)) + (-p - bb)) - pe - n * P3;
+  const double y0 = hi + lo, y1 = lo - (y0 - hi); // r = y0 + y1
+  const double z = y0 * y0;
+  double v;
+  const int q = (int)n & 3;
+  if ((q & 1) == 0) { // k_sin(y0, y1)
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double w = z * y0;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    v = y0 - ((z * (0.5 * y1 - w * r) - y1) - w * S1);
+  } else { // k_cos(y0, y1)
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double zz = z * z;
+    const double r = z * (C1 + z * (C2 + z * C3)) + zz * zz * (C4 + z * (C5 + z * C6));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    v = w + (((1.0 - w) - hz) + (z * r - y0 * y1));
+  }
+  v = (q & 2) ? -v : v;
+  return fabs(x) < 0x1p-26 ? x : v; // sin x = x to 1/2 ulp there; keeps -0
+}
+
 // PerlinNoise::noise + perlin_interp (PerlinNoise.hpp:43-60, 186-201).  The
 // reference's corner weight i*uu + (1-i)*(1-uu) is uu or 1-uu and (u - i) is u or
 // u-1: the same doubles for every input (0*x + y == y, x - 0 == x here; NaN stays
@@ -274,7 +321,11 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
         wgt *= 0.5;
         q = v3(q.x * 2, q.y * 2, q.z * 2);
       }
+#if RT_SIN_N
+      double f = 1 + sin_n(T.scale * p.z + 10 * fabs(acc));
+#else
       double f = 1 + sin(T.scale * p.z + 10 * fabs(acc));
+#endif
       return f * v3(0.5, 0.5, 0.5);
     }
     break;
@@ -558,9 +609,11 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
   return items_closest_t(S, S.bitems, M.b_first, M.b_count, r, thr, kInf, t2);
 }
 
-// ConstantMedium::hit (ConstantMedium.cpp:25-94) in the medium's local frame.
-RT_HD bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tmin,
-                           double tmax, Hit &h, const Key &key, uint32_t bounce) {
+// ConstantMedium::hit (ConstantMedium.cpp:25-94) in the medium's local frame:
+// the scattering distance only (hit_t); medium_record builds the record of
+// the winning medium once, after every medium has been tested.
+RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin,
+                    double tmax, const Key &key, uint32_t bounce, double &hit_t) {
   const DMedium M = S.media[it.idx];
   Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
   double t1, t2;
@@ -575,13 +628,21 @@ RT_HD bool medium_hit(const DScene &S, const DItem &it, const Ray &wr, double tm
   u01x4(key, bounce, kSlotMediumBase + (uint32_t)M.id, uu);
   double hd = M.neg_inv_density * log(uu[0]);
   if (hd > inside) return false;
-  h.t = t1 + hd / rl;
-  h.p = at(r, h.t);
+  hit_t = t1 + hd / rl;
+  return true;
+}
+
+// The record ConstantMedium::hit fills (ConstantMedium.cpp:80-92) at the
+// distance medium_t returned: the same local ray, so the same point.
+RT_HD RT_FI void medium_record(const DScene &S, const DItem &it, const Ray &wr, double t,
+                               Hit &h) {
+  Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
+  h.t = t;
+  h.p = at(r, t);
   h.n = v3(1, 0, 0);
   h.front = true;
-  h.mat = M.phase;
+  h.mat = S.media[it.idx].phase;
   if (it.xf_count) to_world(S, it.xf_first, it.xf_count, h);
-  return true;
 }
 
 // ------------------------------------------------------------ traversal
@@ -758,18 +819,22 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
     const RayF<kFma> q = ray_f32<kFma>(r);
     const float tmin32 = f32_dn(tmin);
     float cl32 = f32_up(closest);
+    int best_m = -1;
     for (int m = 0; m < S.n_mitems; ++m) {
       if (slab(q, S.mbox + 6 * m, S.mbox + 6 * m + 3, tmin32, cl32) == __builtin_huge_valf())
         continue;
       if (STATS) cnt.other++;
-      Hit tmp;
-      if (medium_hit(S, S.mitems[m], r, tmin, closest, tmp, key, bounce)) {
-        closest = tmp.t;
+      double tm_hit;
+      if (medium_t(S, S.mitems[m], r, tmin, closest, key, bounce, tm_hit)) {
+        closest = tm_hit;
         cl32 = f32_up(closest);
-        best = m;
-        best_full = true;
-        h = tmp;
+        best_m = m;
       }
+    }
+    if (best_m >= 0) {
+      medium_record(S, S.mitems[best_m], r, closest, h);
+      best = best_m;
+      best_full = true;
     }
     if (STATS && wave_once()) cnt.cmedia += clk() - t0;
   }

@@ -198,6 +198,12 @@ extern "C" void emu_sincos_2pi(const double *u, int n, double *s, double *c) {
   for (int k = 0; k < n; ++k) rtp::sincos_2pi(u[k], s[k], c[k]);
 }
 
+// sin_n (the noise texture's sin) over n arguments (its accuracy test,
+// tests/test_emulator.py)
+extern "C" void emu_sin_n(const double *x, int n, double *s) {
+  for (int k = 0; k < n; ++k) s[k] = rtp::sin_n(x[k]);
+}
+
 // div_mk (Markstein quotient from a shared reciprocal) over n operand pairs
 // (its bit-exactness test, tests/test_emulator.py)
 extern "C" void emu_div_mk(const double *x, const double *b, int n, double *q) {

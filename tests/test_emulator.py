@@ -143,6 +143,35 @@ def test_sincos_2pi_accuracy(emu):
     assert s[0] == 0.0 and c[0] == 1.0
 
 
+def test_sin_n_within_one_ulp(emu):
+    """sin_n (rt_path.h, NoiseTexture's sin: Cody-Waite reduction + fdlibm
+    kernels below 2^20, the library sin beyond) against sin in long double:
+    at most 1 ulp on random arguments over the noise texture's range and
+    beyond, arguments next to multiples of pi/2 (hardest reductions), tiny,
+    huge, signed zeros and non-finite values."""
+    rng = np.random.default_rng(8)
+    k = rng.integers(-600000, 600000, size=200000).astype(np.float64)
+    near = (k * (np.pi / 2)).astype(np.float64)  # next to multiples of pi/2
+    near = np.concatenate([near, np.nextafter(near, np.inf), np.nextafter(near, -np.inf)])
+    x = np.concatenate([rng.uniform(-4000, 4000, 300000), rng.uniform(-2**20, 2**20, 100000),
+                        rng.uniform(-1, 1, 50000), near,
+                        np.exp2(rng.uniform(-1000, 19.99, 50000)) * rng.choice([-1, 1], 50000),
+                        rng.uniform(2**20, 1e300, 2000), [0.0, -0.0, 2**20, -2**20, np.pi / 4,
+                                                          np.inf, -np.inf, np.nan]])
+    out = np.zeros_like(x)
+    P = C.POINTER(C.c_double)
+    emu.emu_sin_n.argtypes = [P, C.c_int, P]
+    emu.emu_sin_n(x.ctypes.data_as(P), len(x), out.ctypes.data_as(P))
+    fin = np.isfinite(x)
+    assert np.all(np.isnan(out[~fin]))
+    assert out[x == 0].tolist() == [0.0, -0.0] and np.signbit(out[x == 0]).tolist() == [False, True]
+    want = np.sin(x[fin].astype(np.longdouble))
+    ulp = np.spacing(np.abs(want.astype(np.float64)))
+    err = np.abs(out[fin].astype(np.longdouble) - want) / ulp.astype(np.longdouble)
+    assert float(err.max()) <= 1.0, (x[fin][np.argmax(err)], float(err.max()))
+    assert np.all(np.abs(out[fin]) <= 1)
+
+
 def test_div_mk_equals_division(emu):
     """div_mk (rt_path.h: x * RN(1/b) plus one FMA correction, used for the sphere
     roots and ct/pi) returns the IEEE division's double, bit for bit, on random
