@@ -530,18 +530,23 @@ RT_HD bool items_closest_t(const DScene &S, const DItem *its, int first, int n, 
 // of the kept ones passes the second test does the exact second scan run.
 RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, double &t1,
                                double &t2) {
-  // the three smallest candidates, ascending; kK: quad candidate (closed interval)
+  // the three smallest candidates, ascending; bit k of kf: candidate k is a quad
+  // distance (closed interval).  Flags as bits of one integer: three bools
+  // shifted by the insertion were kept in scratch memory by the compiler.
   double c0 = 0, c1 = 0, c2 = 0;
-  bool k0 = false, k1 = false, k2 = false;
+  uint32_t kf = 0;
   int n_cand = 0;
-  auto keep = [&](double t, bool cl) {
+  auto keep = [&](double t, uint32_t cl) {
     ++n_cand;
     if (n_cand == 1 || t < c0) {
-      c2 = c1, k2 = k1, c1 = c0, k1 = k0, c0 = t, k0 = cl;
+      c2 = c1, c1 = c0, c0 = t;
+      kf = ((kf << 1) | cl) & 7u;
     } else if (n_cand == 2 || t < c1) {
-      c2 = c1, k2 = k1, c1 = t, k1 = cl;
+      c2 = c1, c1 = t;
+      kf = (kf & 1u) | (cl << 1) | ((kf & 2u) << 1);
     } else if (n_cand == 3 || t < c2) {
-      c2 = t, k2 = cl;
+      c2 = t;
+      kf = (kf & 3u) | (cl << 2);
     }
   };
   Ray lr = r;
@@ -565,8 +570,8 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
       if (disc < 0) continue;
       double sq = sqrt(disc);
       double r1 = (h - sq) / a, r2 = (h + sq) / a;
-      if (-kInf < r1 && r1 < kInf) keep(r1, false);
-      if (-kInf < r2 && r2 < kInf) keep(r2, false);
+      if (-kInf < r1 && r1 < kInf) keep(r1, 0u);
+      if (-kInf < r2 && r2 < kInf) keep(r2, 0u);
     } else { // quad_t without its interval test
       const DQuad &q = S.quads[it.idx];
       double tt;
@@ -584,24 +589,24 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
         double beta = dot(w, cross(ld3(q.u), pv));
         if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) continue;
       }
-      keep(tt, true);
+      keep(tt, 1u);
     }
   }
   if (n_cand == 0) return false;
   t1 = c0;
   const double thr = t1 + 0.0001;
-  auto pass = [&](double t, bool cl) {
+  auto pass = [&](double t, uint32_t cl) {
     return cl ? (thr <= t && t <= kInf) : (thr < t && t < kInf);
   };
-  if (pass(c0, k0)) {
+  if (pass(c0, kf & 1u)) {
     t2 = c0;
     return true;
   }
-  if (n_cand >= 2 && pass(c1, k1)) {
+  if (n_cand >= 2 && pass(c1, kf & 2u)) {
     t2 = c1;
     return true;
   }
-  if (n_cand >= 3 && pass(c2, k2)) {
+  if (n_cand >= 3 && pass(c2, kf & 4u)) {
     t2 = c2;
     return true;
   }
