@@ -372,7 +372,7 @@ constexpr double kInvPi = 1.0 / kPi; // correctly rounded at compile time
 
 RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tmin,
                                             double tmax, double &root, bool moving = true,
-                                            const double *ya = nullptr) {
+                                            bool mk = false, double ya = 0.0) {
   V3 cc = sphere_center(s, r.tm, moving);
   V3 oc = cc - r.o;
   double h = dot(r.d, oc);
@@ -380,10 +380,10 @@ RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tm
   double disc = h * h - a * c;
   if (disc < 0) return false;
   double sq = sqrt(disc);
-  // ya = RN(1/a) shared by every root of one ray (div_mk), else the division
-  double t = (RT_MK_SPHERE && ya) ? div_mk(h - sq, a, *ya) : (h - sq) / a;
+  // mk: ya = RN(1/a) shared by every root of one ray (div_mk), else the division
+  double t = (RT_MK_SPHERE && mk) ? div_mk(h - sq, a, ya) : (h - sq) / a;
   if (!(tmin < t && t < tmax)) {
-    t = (RT_MK_SPHERE && ya) ? div_mk(h + sq, a, *ya) : (h + sq) / a;
+    t = (RT_MK_SPHERE && mk) ? div_mk(h + sq, a, ya) : (h + sq) / a;
     if (!(tmin < t && t < tmax)) return false;
   }
   root = t;
@@ -896,19 +896,22 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     const DItem it = S.items[ii];
     Ray lr = r;
     double al = a;
-    const double *pya = &ya;
+    bool local = false;
     if constexpr ((F & F_XFORM) != 0) {
       if (it.xf_count) {
         lr = to_local(S, it.xf_first, it.xf_count, r);
         al = len2(lr.d);
-        pya = nullptr; // a local ray has its own |d|^2: plain division
+        local = true;
       }
     }
     double t;
     bool hit;
     if (it.kind == I_SPHERE) {
       if (STATS) cnt.spheres++;
-      hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t, moving, pya);
+      // a local ray has its own |d|^2 and so its own reciprocal (a value, not
+      // a pointer to one of two locals: that pointer kept ya in scratch memory)
+      const double yl = local ? 1.0 / al : ya;
+      hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t, moving, true, yl);
     } else {
       if (STATS) cnt.quads++;
       hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
