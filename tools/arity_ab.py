@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Binary vs 4-wide world BVH walk, A/B interleaved (A B A B ...), on the C3
-scene (bouncing_seed42, 1920x1080 spp 256 depth 50) and on N random spheres
+scene (bouncing_seed42, 1920x1080 spp 256 depth 8) and on N random spheres
 (tools/bvh_build_bench.scene, 1920x1080 spp 4 depth 8).
   python tools/arity_ab.py [--n 20000 100000] [--rounds 3]"""
 import argparse
@@ -50,7 +50,7 @@ def main():
     a = ap.parse_args()
     if not a.no_c3:
         S = load_scene(os.path.join(ROOT, "real-time-ray-tracing-engine_amd", "scenes", "bouncing_seed42.json"))
-        f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=256, max_depth=50))
+        f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=256, max_depth=8))
         ab("C3 bouncing_seed42", S, f, a.rounds)
     for n in a.n:
         S = scene(n)
