@@ -332,6 +332,8 @@ def main():
                          "collective path the driver's multi-GPU runs take on one GPU")
     ap.add_argument("--check", action="store_true",
                     help="rank 0 compares the reduced frame with a 1-device render")
+    ap.add_argument("--pmc-save", default="",
+                    help="write the live PMC summary (the pmc_<config>.json format) here")
     ap.add_argument("--pmc", default="auto", choices=["auto", "file", "off"],
                     help="N=1 roofline counters: auto = rocprofv3 PMC passes of this build "
                          "run before the timed run (fallback: the committed "
@@ -342,6 +344,9 @@ def main():
     pmc = None
     if ws == 1 and args.pmc == "auto":  # before this process initialises the GPU
         pmc = pmc_live(args)
+        if pmc and args.pmc_save:
+            with open(args.pmc_save, "w") as fh:
+                json.dump(dict(pmc, config=args.config), fh, indent=1)
     import torch
     from rtx import abi
     from rtx.render import Renderer, camera_frame
