@@ -317,7 +317,9 @@ int rt_render_device(rt_scene *scene, const rt_frame *frame,
    over every node's two children of area(child) / area(root) x (leaf: its item
    count; inner: 1) -- the tree-quality figure of the reference's builder
    (BVHNode.cpp:215-254, unit traversal and intersection costs).  0 for a flat
-   world.  Copies the nodes back from the device. */
+   world.  Always the BINARY tree the builder made (for a 4-wide scene, the
+   tree before the collapse, costed at creation); otherwise copies the nodes
+   back from the device. */
 int rt_scene_bvh_cost(const rt_scene *scene, double *cost);
 
 /* Run the counter-instrumented kernel variant (untimed) and return totals. */
