@@ -163,7 +163,7 @@ typedef struct rt_scene_desc {
   int32_t bvh_builder; /* RT_BVH_AUTO (0): device binned SAH from 65536 world
                           primitives, host SAH below; RT_BVH_HOST; RT_BVH_DEVICE
                           (linear BVH); RT_BVH_DEVICE_SAH */
-  int32_t bvh_arity;   /* world BVH node width: 0 = auto (4 from 16384 world
+  int32_t bvh_arity;   /* world BVH node width: 0 = auto (4 from 4096 world
                           primitives, else 2), 2, or 4 (the binary tree collapsed
                           to 4-wide nodes) */
 } rt_scene_desc;

@@ -55,7 +55,7 @@ void build_world_bvh_host(HostScene &H);
 
 // Scenes with at least this many world primitives walk a 4-wide BVH when
 // rt_scene_desc.bvh_arity is 0 (auto).
-constexpr int kBvh4Min = 16384;
+constexpr int kBvh4Min = 4096;
 
 // Collapses the binary BFS-ordered tree `bin` (root 0) into 4-wide nodes, BFS
 // order, root 0: each 4-wide node starts from one binary node's two children

@@ -1,6 +1,6 @@
 """4-wide world BVH (RT_FEAT_BVH4; VERDICT r1 item 9: BVH arity per scene size).
 The binary tree (host or device built) is collapsed into 4-wide nodes
-(rt_scene.cpp collapse_bvh4) for scenes of at least kBvh4Min = 16384 world
+(rt_scene.cpp collapse_bvh4) for scenes of at least kBvh4Min = 4096 world
 primitives, or when rt_scene_desc.bvh_arity asks for it.  The closest hit does
 not depend on the tree, so images equal the binary walk's (1e-12: an exact tie
 between two surfaces may resolve the other way round) and the oracle's."""
