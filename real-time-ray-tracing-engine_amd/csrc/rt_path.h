@@ -1162,6 +1162,15 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 // L = e + a*L' sums emission only where a path ends (lights never scatter), so the
 // forward form needs no radiance register: the terminal T x value is the sample.
 // The material half of a segment, after the closest hit `h` of ps.ray.
+#ifndef RT_SHADE_MERGE
+#define RT_SHADE_MERGE 1
+#endif
+// Measured (profiles/r02w_shade_merge_ab.log): C3 (plain BVH instance, mixed
+// Lambertian / metal / glass) +2 %; C2 (flat, Lambertian only: the selects are
+// pure overhead) -2 %, C4 -1 % (more spills): merged in the plain BVH instances only.
+#ifndef RT_SHADE_MERGE_F
+#define RT_SHADE_MERGE_F(F) (RT_SHADE_MERGE != 0 && ((F) & ~F_BVH4) == 0)
+#endif
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
                        const Hit &h, Counters &cnt) {
@@ -1180,7 +1189,61 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
-  if (M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
+  constexpr bool kMerge = RT_SHADE_MERGE_F(F);
+  // Merged shading (kMerge): a wave whose lanes shade different materials
+  // runs each material's branch; the expensive steps they have in common run
+  // ONCE for all lanes here, each lane feeding its own operand -- the same
+  // operations on the same values as in the per-material code below:
+  //   unit vector: metal's reflection, the dielectric's ray, the ONB normal;
+  //   sincos(2 pi a): metal / isotropic a = d1, Lambertian a = d0;
+  //   first root: metal / isotropic 1 - z^2 (>= 0), Lambertian d1, dielectric
+  //   1 - ct^2.
+  V3 u1{};
+  double sp1 = 0.0, cp1 = 0.0, s1 = 0.0, z1 = 0.0, ct1 = 0.0;
+  if constexpr (kMerge) {
+    const bool metal = M.kind == RT_MAT_METAL, diel = M.kind == RT_MAT_DIELECTRIC;
+    const bool lamb = M.kind == RT_MAT_LAMBERTIAN;
+    V3 x1 = diel ? r.d : h.n;
+    if (metal) x1 = r.d - (2 * dot(r.d, h.n)) * h.n;
+    u1 = unitv(x1);
+    if (!diel) sincos_2pi(lamb ? d0 : d1, sp1, cp1);
+    z1 = 1.0 - 2.0 * d0;
+    if (diel) ct1 = fmin(dot(-u1, h.n), 1.0);
+    s1 = sqrt_n(lamb ? d1 : (diel ? 1.0 - ct1 * ct1 : fmax(0.0, 1.0 - z1 * z1)));
+  }
+  if (kMerge && M.kind == RT_MAT_METAL) {
+    if (STATS) cnt.wshade += wave_once();
+    V3 uv = v3(s1 * cp1, s1 * sp1, z1);
+    V3 refl = u1 + (M.fuzz * uv);
+    ps.T = ps.T * ld3(M.albedo);
+    ps.ray = Ray{h.p, refl, r.tm};
+    return advance(ps, C);
+  }
+  if (kMerge && M.kind == RT_MAT_DIELECTRIC) {
+    if (STATS) cnt.wshade += wave_once();
+    double ri = h.front ? M.inv_ior : M.ior;
+    const V3 ud = u1;
+    const double ct = ct1, st = s1;
+    bool reflect_it = ri * st > 1.0;
+    if (!reflect_it) {
+      const double r0 = h.front ? M.r0[0] : M.r0[1];
+      double x = 1 - ct;
+      double x2 = x * x;
+      double refl = r0 + (1 - r0) * (x2 * x2 * x);
+      reflect_it = refl > e0;
+    }
+    V3 dir;
+    if (reflect_it) {
+      dir = ud - (2 * dot(ud, h.n)) * h.n;
+    } else {
+      V3 perp = ri * (ud + ct * h.n);
+      V3 par = (-sqrt_n(fabs(1.0 - len2(perp)))) * h.n;
+      dir = perp + par;
+    }
+    ps.ray = Ray{h.p, dir, r.tm};
+    return advance(ps, C);
+  }
+  if (!kMerge && M.kind == RT_MAT_METAL) { // MetalMaterial.cpp:43-62
     if (STATS) cnt.wshade += wave_once();
     V3 refl = r.d - (2 * dot(r.d, h.n)) * h.n;
     double z = 1.0 - 2.0 * d0;
@@ -1193,7 +1256,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     ps.ray = Ray{h.p, refl, r.tm};
     return advance(ps, C);
   }
-  if (M.kind == RT_MAT_DIELECTRIC) { // DielectricMaterial.cpp:58-85
+  if (!kMerge && M.kind == RT_MAT_DIELECTRIC) { // DielectricMaterial.cpp:58-85
     if (STATS) cnt.wshade += wave_once();
     double ri = h.front ? M.inv_ior : M.ior; // 1/ior formed on the host
     V3 ud = unitv(r.d);
@@ -1225,7 +1288,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   // overlaps less live state there), late otherwise (shorter live range)
   V3 att;
   if constexpr ((F & F_NOISE) != 0) att = tex_value<F>(S, M.tex, h.p);
-  V3 w = unitv(h.n); // ONB(n), ONB.hpp:25-37
+  V3 w = kMerge ? u1 : unitv(h.n); // ONB(n), ONB.hpp:25-37
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
   V3 ov = unitv(cross(w, a));
   V3 ou = cross(w, ov);
@@ -1242,7 +1305,14 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     }
   }
   if (!from_light) {
-    if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
+    if (kMerge) { // the shared sincos and first root (above)
+      if (lamb) {
+        V3 lc = v3(cp1 * s1, sp1 * s1, sqrt_n(1 - d1));
+        gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
+      } else {
+        gd = v3(s1 * cp1, s1 * sp1, z1);
+      }
+    } else if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
       double sp, cp;
       sincos_2pi(d0, sp, cp);
       double sr = sqrt_n(d1);
