@@ -250,6 +250,9 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   std::string err;
   int rc = rtx::compile_scene(desc, H, err);
   if (rc != RT_OK) return set_err(rc, err);
+  // the compacted leaf tests pack (item << 6 | lane) into an int (rt_path.h leaf_share)
+  if (H.items.size() >= ((size_t)1 << 25))
+    return set_err(RT_ERR_UNSUPPORTED, "more than 2^25 - 1 world primitives");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hip_err(e, "hipGetDeviceCount");

@@ -70,6 +70,8 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
   extern __shared__ int4 dyn_lds[];
   __shared__ double acc_lds[kWaves][64][3];
+  // compacted leaf tests (BVH instances only; 1 KB per wave)
+  __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? kWaves : 1];
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -142,7 +144,8 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt);
+      bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt,
+                                    (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0]);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);

@@ -775,6 +775,30 @@ RT_HD RT_FI float slab(const RayF<FMA> &q, const float *lo, const float *hi, flo
     return tl <= th * kSlabGrow ? tl : __builtin_huge_valf();
 }
 
+// Per-wave LDS scratch of the compacted leaf tests (trace, leaf_share): the
+// round's (item << 6 | owner lane) table and each owner's running closest t
+// (as order-preserving bits: every t is positive), its tie key and its item.
+struct LeafPool {
+  unsigned long long bt[64];
+  int bk[64]; // tie key of the owner's current hit (leaf_share)
+  int bi[64];
+  int tab[64];
+};
+// Which instances compact their leaf tests across the wave (BVH walks only; a
+// flat world's items are wave-uniform already).  Off in the product build:
+// measured C3 -11 % (-19 % when every leaf phase compacts), since moving a ray
+// between lanes (9 doubles through ds_bpermute) plus the LDS merge costs about
+// as much as the sphere test it saves, and leaf-phase lane use rose only
+// 0.39 -> 0.52 (profiles/r02y_*, r02z_*).  Built as the variant
+// build/variants/librtx_hip_leafshare.so, parity-tested on the GPU
+// (tests/test_leaf_share.py).
+#ifndef RT_LEAF_SHARE
+#define RT_LEAF_SHARE 0
+#endif
+#ifndef RT_LEAF_SHARE_F
+#define RT_LEAF_SHARE_F(F) (RT_LEAF_SHARE != 0 && ((F) & F_FLAT) == 0)
+#endif
+
 struct Counters {
   uint32_t nodes, spheres, quads, other, light, shade;
   uint32_t wnode, wleaf, wshade; // wave-level iterations (counted by one lane per wave)
@@ -870,7 +894,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                                       uint32_t bounce, int *stk, const RT_LDS DNode *lnodes,
-                                      Counters &cnt) {
+                                      Counters &cnt, RT_LDS LeafPool *pool = nullptr) {
   const double tmin = 0.001; // Camera.cpp:242
   double closest = kInf;
   int best = -1;
@@ -890,38 +914,128 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     q = ray_f32<kFma>(r);
     tmin32 = f32_dn(tmin);
   }
-  // closest-hit test of one world item (records only t and the item index)
-  auto test_item = [&](int ii) {
-    if (STATS) cnt.wleaf += wave_once();
+  // hit test of world item ii against ray rr (|d|^2 = ra, its reciprocal ry)
+  // in (tmin, tmax): the root in t
+  auto item_root = [&](int ii, const Ray &rr, double ra, double ry, double tmax,
+                       double &t) -> bool {
     const DItem it = S.items[ii];
-    Ray lr = r;
-    double al = a;
+    Ray lr = rr;
+    double al = ra;
     bool local = false;
     if constexpr ((F & F_XFORM) != 0) {
       if (it.xf_count) {
-        lr = to_local(S, it.xf_first, it.xf_count, r);
+        lr = to_local(S, it.xf_first, it.xf_count, rr);
         al = len2(lr.d);
         local = true;
       }
     }
-    double t;
-    bool hit;
     if (it.kind == I_SPHERE) {
       if (STATS) cnt.spheres++;
       // a local ray has its own |d|^2 and so its own reciprocal (a value, not
       // a pointer to one of two locals: that pointer kept ya in scratch memory)
-      const double yl = local ? 1.0 / al : ya;
-      hit = sphere_root(S.spheres[it.idx], lr, al, tmin, closest, t, moving, true, yl);
-    } else {
-      if (STATS) cnt.quads++;
-      hit = quad_t(S.quads[it.idx], lr, tmin, closest, t);
+      const double yl = local ? 1.0 / al : ry;
+      return sphere_root(S.spheres[it.idx], lr, al, tmin, tmax, t, moving, true, yl);
     }
+    if (STATS) cnt.quads++;
+    return quad_t(S.quads[it.idx], lr, tmin, tmax, t);
+  };
+  // closest-hit test of one world item (records only t and the item index)
+  auto test_item = [&](int ii) {
+    if (STATS) cnt.wleaf += wave_once();
+    double t;
+    const bool hit = item_root(ii, r, a, ya, closest, t);
     if (hit) {
       closest = t;
       if constexpr (kBoxes) cl32 = f32_up(closest);
       best = ii;
     }
   };
+
+  constexpr bool kShare = RT_LEAF_SHARE_F(F);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Leaf tests compacted with ballot + ds_bpermute: the lanes' parked leaves
+  // (ln items from lf) are numbered by a ballot prefix sum; each round, every
+  // lane of the query takes the next item number, reads (item, owner) from the
+  // wave's LDS table, borrows the owner's ray with ds_bpermute and tests it
+  // against the owner's current bound; hits are merged per owner in LDS.  The
+  // merge reproduces the per-lane loop over the leaf exactly: the smallest t
+  // wins, and among equal t the loop's replacement rules decide -- a sphere
+  // replaces the closest hit only on t < closest (Sphere.cpp), a quad also on
+  // t == closest (Plane.cpp's closed interval) -- so the winner is the last
+  // quad in item order at that t, else the first sphere, and a quad at the
+  // previous closest t replaces the previous hit while a sphere does not.
+  // Tie keys: quad 2^26-1-item < previous hit 2^26 < sphere 2^26+1+item.
+  auto leaf_share = [&](int &ln_, int &lf_) {
+    constexpr int kPrev = 1 << 26;
+    const int lane = (int)__lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t ex = __ballot(1);
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) { // counts are <= 7 (3-bit leaf field)
+      const uint64_t m = __ballot((ln_ >> b) & 1);
+      pre += __popcll(m & below) << b;
+      tot += __popcll(m) << b;
+    }
+    const int nx = __popcll(ex), rk = __popcll(ex & below);
+    unsigned long long cbits = (unsigned long long)__double_as_longlong(closest);
+    int ckey = kPrev;
+    pool->bt[lane] = cbits;
+    pool->bk[lane] = kPrev;
+    for (int base = 0; base < tot; base += nx) {
+      if (STATS) cnt.wleaf += wave_once();
+      for (int k = base > pre ? base - pre : 0; k < ln_ && pre + k < base + nx; ++k)
+        pool->tab[pre + k - base] = ((lf_ + k) << 6) | lane;
+      __builtin_amdgcn_wave_barrier();
+      const int w = base + rk;
+      int o = lane, ii = 0;
+      if (w < tot) {
+        const int e = pool->tab[rk];
+        o = e & 63;
+        ii = e >> 6;
+      }
+      Ray ro;
+      ro.o = v3(__shfl(r.o.x, o), __shfl(r.o.y, o), __shfl(r.o.z, o));
+      ro.d = v3(__shfl(r.d.x, o), __shfl(r.d.y, o), __shfl(r.d.z, o));
+      ro.tm = __shfl(r.tm, o);
+      const double ra = __shfl(a, o), ry = __shfl(ya, o);
+      bool hit = false;
+      double t = 0.0;
+      unsigned long long tb = 0;
+      int key = 0;
+      if (w < tot) {
+        const double tmax = __longlong_as_double((long long)pool->bt[o]);
+        hit = item_root(ii, ro, ra, ry, tmax, t);
+        tb = (unsigned long long)__double_as_longlong(t);
+        key = S.items[ii].kind == I_SPHERE ? kPrev + 1 + ii : kPrev - 1 - ii;
+        if (hit)
+          __hip_atomic_fetch_min(&pool->bt[o], tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // a new closest t: the previous hit's key no longer competes
+      if (pool->bt[lane] != cbits) pool->bk[lane] = 0x7fffffff;
+      __builtin_amdgcn_wave_barrier();
+      const bool at_min = hit && pool->bt[o] == tb;
+      if (at_min)
+        __hip_atomic_fetch_min(&pool->bk[o], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __builtin_amdgcn_wave_barrier();
+      if (at_min && pool->bk[o] == key) pool->bi[o] = ii; // keys are unique per item
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long nb = pool->bt[lane];
+      const int nk = pool->bk[lane];
+      if (nb != cbits || nk != ckey) {
+        cbits = nb;
+        ckey = nk;
+        closest = __longlong_as_double((long long)nb);
+        best = pool->bi[lane];
+        if constexpr (kBoxes) cl32 = f32_up(closest);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    lf_ += ln_;
+    ln_ = 0;
+  };
+#endif
 
   if constexpr (kFlat) {
     // the reference's HittableList walk (HittableList.cpp), wave-uniform items
@@ -1043,12 +1157,42 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           cur = sp > 0 ? stk[64 * --sp] : -1;
         }
       }
-      if (ln == 0) break; // nothing parked and nothing left to walk: done
-      while (ln > 0) { // ---- the single leaf-test site
-        const int ii = lf;
-        ++lf;
-        --ln;
-        test_item(ii);
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (kShare) {
+        // ---- the single leaf-test site, compacted across the wave: every
+        // lane of the query (finished walks included) tests one of the wave's
+        // parked leaf items per round instead of its own leaf's items in turn
+        if (__ballot(ln > 0) == 0) break; // no lane holds a leaf: all walks done
+        // compact only when it takes fewer rounds than the per-lane loop's
+        // max(ln) trips (each round also moves rays between lanes)
+        int mx = 1;
+#pragma unroll
+        for (int k = 2; k <= 7; ++k)
+          if (__ballot(ln >= k) != 0) mx = k;
+        int tot = 0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) tot += __popcll(__ballot((ln >> b) & 1)) << b;
+        const int nx = __popcll(__ballot(1));
+        if ((tot + nx - 1) / nx < mx) {
+          leaf_share(ln, lf);
+        } else {
+          while (ln > 0) {
+            const int ii = lf;
+            ++lf;
+            --ln;
+            test_item(ii);
+          }
+        }
+      } else
+#endif
+      {
+        if (ln == 0) break; // nothing parked and nothing left to walk: done
+        while (ln > 0) { // ---- the single leaf-test site
+          const int ii = lf;
+          ++lf;
+          --ln;
+          test_item(ii);
+        }
       }
       if (cur < -1) { // a second leaf met while one was parked: it is next
         lf = (~cur) >> 3;
@@ -1363,10 +1507,10 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
                                         const Key &key, int *stk, const RT_LDS DNode *lnodes,
-                                        Counters &cnt) {
+                                        Counters &cnt, RT_LDS LeafPool *pool = nullptr) {
   Hit h;
   const uint64_t t0 = STATS ? clk() : 0;
-  const bool hit = trace<STATS, F>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt);
+  const bool hit = trace<STATS, F>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt, pool);
   const uint64_t t1 = STATS ? clk() : 0;
   if (STATS && wave_once()) cnt.ctrace += t1 - t0;
   if (!hit) {
