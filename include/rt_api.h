@@ -40,8 +40,8 @@
  *
  * Threading.  Distinct rt_scene objects are independent and may be used from
  * different host threads (and devices) at once.  One rt_scene is used by one
- * host thread at a time: its kernel-timing events and its scratch / staging
- * buffers are per scene.  Asynchronous launches (rt_render_device) on one
+ * host thread at a time: its kernel-timing events, its scratch / staging
+ * buffers and its work-unit counter (persistent launches) are per scene.  Asynchronous launches (rt_render_device) on one
  * scene must be ordered by the caller's streams as any device work is.
  *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The

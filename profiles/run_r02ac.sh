@@ -1,0 +1,11 @@
+#!/bin/bash
+# r02ac: persistent waves only in the plain BVH instances (base) vs the
+# previous product build (L0 = one unit per wave everywhere): parity + A/B
+set -o pipefail
+O=gpurun_out/r02ac
+mkdir -p $O
+export PYTHONPATH=$PWD/real-time-ray-tracing-engine_amd:$PWD/tests:$PWD
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_instances.py tests/test_bvh4.py tests/test_multi.py tests/test_device_bvh.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+bash profiles/ab_variants.sh base L0 base L0 > $O/ab.log 2>&1 || exit 1
+cat $O/ab.log

@@ -54,6 +54,7 @@ struct rt_scene {
   double *out_buf = nullptr; // rt_render staging
   size_t out_bytes = 0;
   unsigned long long *stats = nullptr;
+  int32_t *unit_ctr = nullptr; // work-unit counter of persistent launches (scene block)
   double *scratch = nullptr; // chunk partials of chunked frame launches
   size_t scratch_bytes = 0;
   int wave_slots = 0;        // resident waves of the render instance on this device
@@ -158,6 +159,8 @@ int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
     return set_err(RT_ERR_UNSUPPORTED, "too many work units");
   L.n_chunks = chunks;
   L.chunk_strata = (L.sample_count + chunks - 1) / chunks;
+  L.unit_ctr = nullptr;
+  L.grid_cap = 0;
   return RT_OK;
 }
 
@@ -295,6 +298,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   size_t iP = add(H.perlin.data(), H.perlin.size() * sizeof(DPerlin));
   size_t iLi = add(H.lights.data(), H.lights.size() * sizeof(DLight));
   size_t iSt = add(nullptr, RT_N_STATS * sizeof(unsigned long long));
+  size_t iUc = add(nullptr, sizeof(int32_t));
 
   rt_scene *s = new rt_scene();
   s->device = device;
@@ -438,6 +442,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
   }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
+  s->unit_ctr = (int32_t *)(s->block + parts[iUc].off);
 
   rt_scene_info &in = s->info;
   std::memset(&in, 0, sizeof in);
@@ -516,10 +521,21 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
     int rc = ensure_scratch(s, (size_t)L.n_local_tiles * chunks * 64 * 3 * sizeof(double));
     if (rc) return rc;
   }
+  // persistent waves pulling work units (RT_PERSISTENT=0 in the environment:
+  // one unit per wave, for A/B runs)
+  static const bool persistent = [] {
+    const char *v = getenv("RT_PERSISTENT");
+    return !(v && v[0] == '0');
+  }();
+  DLaunch Lp = L;
+  if (persistent && s->wave_slots > 0) {
+    Lp.unit_ctr = s->unit_ctr;
+    Lp.grid_cap = std::max(1, s->wave_slots / 4);
+  }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
-  e = chunks > 1 ? rtk_launch_render_chunked(&s->ds, &C, &L, chunks, dev_out, s->scratch, st)
-                 : rtk_launch_render(&s->ds, &C, &L, dev_out, stats, st);
+  e = chunks > 1 ? rtk_launch_render_chunked(&s->ds, &C, &Lp, chunks, dev_out, s->scratch, st)
+                 : rtk_launch_render(&s->ds, &C, &Lp, dev_out, stats, st);
   if (e != hipSuccess) return hip_err(e, "render kernel launch");
   e = hipEventRecord(s->ev1, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");

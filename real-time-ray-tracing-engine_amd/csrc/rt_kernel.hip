@@ -61,6 +61,12 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 4
 #endif
+// Instances whose waves persist and pull work units from a counter (the plain
+// BVH walks: C3 +3.7 %, profiles/r02ab_*); the flat and the rich instances keep
+// one unit per wave -- the unit loop's extra live state cost them 2-20 %.
+#ifndef RT_PERSIST_F
+#define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0)
+#endif
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 
 template <bool STATS, unsigned F>
@@ -86,24 +92,32 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
   }
-  const int unit = blockIdx.x * kWaves + wv; // work unit = (local tile, stratum chunk)
-  if (unit >= P.n_local_tiles * P.n_chunks) return; // whole wave exits together
+  // work unit = (local tile, stratum chunk).  Persistent launches (P.unit_ctr
+  // set, grid = the resident waves): a wave's first unit is its static slot,
+  // the next ones come from the agent-scope counter (initialised by the host to
+  // the grid's wave count), each fetched while the current unit runs, so waves
+  // take new units as they finish instead of waiting for their block.
+  const int n_units = P.n_local_tiles * P.n_chunks;
+  int unit = blockIdx.x * kWaves + wv;
+  int *stk = stack_base + wv * S.stack_depth * 64 + lane;
+  double *acc = &acc_lds[wv][0][0];
+  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t cyc_regen = 0;
+  const uint64_t t_start = STATS ? clk() : 0;
+  uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
+  while (unit < n_units) { // wave-uniform
+  int next = n_units;
+  if (RT_PERSIST_F(F) && P.unit_ctr != nullptr && lane == 0)
+    next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int local_tile = unit / P.n_chunks, chunk = unit - local_tile * P.n_chunks;
   const int tile = P.tile_first + local_tile * P.tile_stride;
   const int s_first = P.sample_begin + chunk * P.chunk_strata;
   const int s_count = min(P.chunk_strata, P.sample_count - chunk * P.chunk_strata);
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
   const int x0 = tx * 8, y0 = P.row_begin + ty * 8;
-  int *stk = stack_base + wv * S.stack_depth * 64 + lane;
-  double *acc = &acc_lds[wv][0][0];
   acc[lane * 3 + 0] = 0.0;
   acc[lane * 3 + 1] = 0.0;
   acc[lane * 3 + 2] = 0.0;
-
-  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t cyc_regen = 0;
-  const uint64_t t_start = STATS ? clk() : 0;
-  uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
 
   const int n_items = 64 * max(0, s_count);
   int next_item = 0; // wave-uniform head of the tile's work queue
@@ -179,6 +193,10 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (!RT_PERSIST_F(F)) break;
+  unit = P.unit_ctr != nullptr ? __builtin_amdgcn_readfirstlane(__shfl(next, 0)) : n_units;
+  } // unit loop
   if (STATS) {
     const uint64_t cyc_loop = clk() - t_start;
     unsigned long long v[RT_N_STATS] = {n_samples, n_segments, cnt.nodes, cnt.spheres,
@@ -277,7 +295,18 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, *P, out, stats);
+  DLaunch Q = *P;
+  if (RT_PERSIST_F((unsigned)(S->features & F_ALL)) && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
+      blocks > Q.grid_cap) {
+    // persistent: the resident blocks' waves take units [0, grid_cap * kWaves)
+    // statically, the rest from the counter
+    blocks = Q.grid_cap;
+    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * kWaves, 1, stream);
+    if (e != hipSuccess) return e;
+  } else {
+    Q.unit_ctr = nullptr; // every unit has its own wave
+  }
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, Q, out, stats);
   return hipGetLastError();
 }
 

@@ -192,6 +192,8 @@ struct DLaunch {
   int32_t n_local_tiles;           // k in [0, n_local_tiles)
   int32_t compact;                 // RT_LAYOUT_TILES output
   int32_t n_chunks, chunk_strata;  // work unit = (tile, stratum chunk); compact only
+  int32_t *unit_ctr;               // persistent launch: next work unit (device counter), or null
+  int32_t grid_cap;                // persistent launch: resident blocks of the instance (0: none)
 };
 
 #endif

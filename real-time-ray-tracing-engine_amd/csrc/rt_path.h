@@ -951,7 +951,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     }
   };
 
-  constexpr bool kShare = RT_LEAF_SHARE_F(F);
+  [[maybe_unused]] constexpr bool kShare = RT_LEAF_SHARE_F(F);
 #if defined(__HIP_DEVICE_COMPILE__)
   // Leaf tests compacted with ballot + ds_bpermute: the lanes' parked leaves
   // (ln items from lf) are numbered by a ballot prefix sum; each round, every
