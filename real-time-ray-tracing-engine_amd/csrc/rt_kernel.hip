@@ -64,6 +64,12 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 // Instances whose waves persist and pull work units from a counter (the plain
 // BVH walks: C3 +3.7 %, profiles/r02ab_*); the flat and the rich instances keep
 // one unit per wave -- the unit loop's extra live state cost them 2-20 %.
+// 0: lane 0 fetches the next unit when the current one ends (one atomic
+// round trip per unit of ~3 ms); 1: when it starts, one more register across
+// the unit (measured C3 -0.5 %, profiles/r02ae_unit_prefetch_ab.log)
+#ifndef RT_UNIT_PREFETCH
+#define RT_UNIT_PREFETCH 0
+#endif
 #ifndef RT_PERSIST_F
 #define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0)
 #endif
@@ -95,8 +101,8 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   // work unit = (local tile, stratum chunk).  Persistent launches (P.unit_ctr
   // set, grid = the resident waves): a wave's first unit is its static slot,
   // the next ones come from the agent-scope counter (initialised by the host to
-  // the grid's wave count), each fetched while the current unit runs, so waves
-  // take new units as they finish instead of waiting for their block.
+  // the grid's wave count), so waves take new units as they finish instead of
+  // waiting for their block.
   const int n_units = P.n_local_tiles * P.n_chunks;
   int unit = blockIdx.x * kWaves + wv;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
@@ -106,9 +112,11 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   const uint64_t t_start = STATS ? clk() : 0;
   uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
   while (unit < n_units) { // wave-uniform
+#if RT_UNIT_PREFETCH
   int next = n_units;
   if (RT_PERSIST_F(F) && P.unit_ctr != nullptr && lane == 0)
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   const int local_tile = unit / P.n_chunks, chunk = unit - local_tile * P.n_chunks;
   const int tile = P.tile_first + local_tile * P.tile_stride;
   const int s_first = P.sample_begin + chunk * P.chunk_strata;
@@ -195,6 +203,11 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   }
   __builtin_amdgcn_wave_barrier();
   if constexpr (!RT_PERSIST_F(F)) break;
+#if !RT_UNIT_PREFETCH
+  int next = n_units;
+  if (P.unit_ctr != nullptr && lane == 0)
+    next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   unit = P.unit_ctr != nullptr ? __builtin_amdgcn_readfirstlane(__shfl(next, 0)) : n_units;
   } // unit loop
   if (STATS) {
