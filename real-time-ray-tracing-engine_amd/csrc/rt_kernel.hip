@@ -61,9 +61,10 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_WAVES_FLAT
 #define RT_WAVES_FLAT 4
 #endif
-// Instances whose waves persist and pull work units from a counter (the plain
-// BVH walks: C3 +3.7 %, profiles/r02ab_*); the flat and the rich instances keep
-// one unit per wave -- the unit loop's extra live state cost them 2-20 %.
+// Feature sets with a persistent chunked-frame instance (render_tiles<.., PC>,
+// whose waves pull work units from a counter): the plain BVH walks (C3 +3.4 %,
+// profiles/r02ab-af_*); the flat and the rich instances keep one unit per wave
+// -- the unit loop's extra live state cost them 2-20 %.
 // 0: lane 0 fetches the next unit when the current one ends (one atomic
 // round trip per unit of ~3 ms); 1: when it starts, one more register across
 // the unit (measured C3 -0.5 %, profiles/r02ae_unit_prefetch_ab.log)
@@ -75,7 +76,11 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #endif
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 
-template <bool STATS, unsigned F>
+// PC ("persistent, chunked"): the instance for frame launches split into
+// stratum chunks (rtk_launch_render_chunked: tiles 0.., compact partials, plain
+// sums), whose waves persist and pull units; the launch fields those launches
+// fix are constants here, so they are not live across the path loop.
+template <bool STATS, unsigned F, bool PC = false>
 __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   // dynamic LDS: traversal stacks [kWaves][S.stack_depth][64] ints, then the
@@ -114,11 +119,11 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   while (unit < n_units) { // wave-uniform
 #if RT_UNIT_PREFETCH
   int next = n_units;
-  if (RT_PERSIST_F(F) && P.unit_ctr != nullptr && lane == 0)
+  if (PC && P.unit_ctr != nullptr && lane == 0)
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   const int local_tile = unit / P.n_chunks, chunk = unit - local_tile * P.n_chunks;
-  const int tile = P.tile_first + local_tile * P.tile_stride;
+  const int tile = PC ? local_tile : P.tile_first + local_tile * P.tile_stride;
   const int s_first = P.sample_begin + chunk * P.chunk_strata;
   const int s_count = min(P.chunk_strata, P.sample_count - chunk * P.chunk_strata);
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
@@ -181,16 +186,17 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   // ---- tile epilogue: one coalesced store per pixel
   {
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
-    if (P.compact || (i < C.W && j < P.row_end)) { // tile slots outside the image hold 0
+    const bool compact = PC || P.compact;
+    if (compact || (i < C.W && j < P.row_end)) { // tile slots outside the image hold 0
       double sx = acc[lane * 3 + 0], sy = acc[lane * 3 + 1], sz = acc[lane * 3 + 2];
-      if (P.output == RT_OUT_SCALED) {
+      if (!PC && P.output == RT_OUT_SCALED) {
         sx = C.scale * sx;
         sy = C.scale * sy;
         sz = C.scale * sz;
       }
-      double *o = P.compact ? out + 3 * ((size_t)unit * 64 + lane)
+      double *o = compact ? out + 3 * ((size_t)unit * 64 + lane)
                             : out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
-      if (P.accumulate) {
+      if (!PC && P.accumulate) {
         o[0] += sx;
         o[1] += sy;
         o[2] += sz;
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     }
   }
   __builtin_amdgcn_wave_barrier();
-  if constexpr (!RT_PERSIST_F(F)) break;
+  if constexpr (!PC) break;
 #if !RT_UNIT_PREFETCH
   int next = n_units;
   if (P.unit_ctr != nullptr && lane == 0)
@@ -264,6 +270,11 @@ constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequen
   return {render_tiles<STATS, canonical(Fs)>...};
 }
 
+// the persistent chunked instances (RT_PERSIST_F feature sets)
+RenderFn persistent_instance(unsigned f) {
+  return (f & F_BVH4) ? render_tiles<false, F_BVH4, true> : render_tiles<false, 0u, true>;
+}
+
 // one instance per feature set (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE | F_FLAT)
 const RenderFn *render_table(bool stats) {
   static constexpr auto plain = instance_table<false>(std::make_integer_sequence<unsigned, F_ALL + 1>{});
@@ -309,10 +320,13 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
   DLaunch Q = *P;
-  if (RT_PERSIST_F((unsigned)(S->features & F_ALL)) && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
-      blocks > Q.grid_cap) {
+  const unsigned f = (unsigned)(S->features & F_ALL);
+  if (RT_PERSIST_F(f) && stats == nullptr && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
+      blocks > Q.grid_cap && Q.compact && Q.output == RT_OUT_SUM && !Q.accumulate &&
+      Q.tile_first == 0 && Q.tile_stride == 1) {
     // persistent: the resident blocks' waves take units [0, grid_cap * kWaves)
     // statically, the rest from the counter
+    fn = persistent_instance(f);
     blocks = Q.grid_cap;
     hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * kWaves, 1, stream);
     if (e != hipSuccess) return e;
