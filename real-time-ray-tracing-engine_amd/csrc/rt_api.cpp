@@ -531,6 +531,9 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   if (persistent && s->wave_slots > 0) {
     Lp.unit_ctr = s->unit_ctr;
     Lp.grid_cap = std::max(1, s->wave_slots / 4);
+    // RT_GRID_CAP: fewer resident blocks (tests: many units per wave)
+    if (const char *g = getenv("RT_GRID_CAP"))
+      if (atoi(g) > 0) Lp.grid_cap = atoi(g);
   }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");

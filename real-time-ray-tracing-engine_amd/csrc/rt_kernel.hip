@@ -71,8 +71,11 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_UNIT_PREFETCH
 #define RT_UNIT_PREFETCH 0
 #endif
+#ifndef RT_PERSIST_FLAT
+#define RT_PERSIST_FLAT 0
+#endif
 #ifndef RT_PERSIST_F
-#define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0)
+#define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0 || (RT_PERSIST_FLAT && (F) == F_FLAT))
 #endif
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 
@@ -272,6 +275,9 @@ constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequen
 
 // the persistent chunked instances (RT_PERSIST_F feature sets)
 RenderFn persistent_instance(unsigned f) {
+  if constexpr (RT_PERSIST_F(F_FLAT)) {
+    if (f == F_FLAT) return render_tiles<false, F_FLAT, true>;
+  }
   return (f & F_BVH4) ? render_tiles<false, F_BVH4, true> : render_tiles<false, 0u, true>;
 }
 
