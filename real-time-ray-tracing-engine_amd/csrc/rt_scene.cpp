@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <limits>
@@ -25,6 +26,11 @@
 
 namespace rtx {
 namespace {
+
+int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
 
 const double kInf = std::numeric_limits<double>::infinity();
 const double kPi = 3.1415926535897932385;
@@ -111,6 +117,22 @@ struct SahBuilder {
   };
   std::vector<BNode> bn;
   int max_depth_seen = 0;
+  // Leaf rules: a range of <= leaf_max items is a leaf; one of <= leaf_split
+  // items is a leaf when splitting does not pay (SAH, traversal cost
+  // trav_cost, intersection cost 1).  Binary-walk scenes (< kBvh4Min items)
+  // use single-item leaves: the wave tests leaves together, so a lane's
+  // second leaf item costs the whole wave a trip (C3: 2 / 4 -> 1 / 1 gave
+  // +2.1 %, profiles/r02aj_sah_leaf_sweep.log); the 4-wide and device-built
+  // trees keep 2 / 4 (the device SAH builder's rules).  Measurement overrides:
+  // RT_SAH_LEAF_MAX, RT_SAH_LEAF_SPLIT, RT_SAH_TRAV_X4 (4 x trav_cost).
+  int leaf_max = 2, leaf_split = 4;
+  double trav_cost = 1.0;
+  void set_leaf_rules(size_t n_items) {
+    const bool binary = n_items < (size_t)kBvh4Min;
+    leaf_max = env_int("RT_SAH_LEAF_MAX", binary ? 1 : 2);
+    leaf_split = env_int("RT_SAH_LEAF_SPLIT", binary ? 1 : 4);
+    trav_cost = env_int("RT_SAH_TRAV_X4", 4) / 4.0;
+  }
 
   int build(std::vector<BRef> &r, int st, int en, int dep) {
     BNode n;
@@ -125,7 +147,8 @@ struct SahBuilder {
     max_depth_seen = std::max(max_depth_seen, dep);
     int id = (int)bn.size();
     bn.push_back(n);
-    const int kLeafMax = 2;
+    const int kLeafMax = leaf_max, kLeafSplit = leaf_split;
+    const double kTrav = trav_cost;
     // A small world is one flat leaf (the reference's own HittableList walk,
     // in list order): a wavefront's lanes scatter over the whole scene, so a
     // split of a handful of items only adds a node visit and divergent leaf
@@ -196,7 +219,7 @@ struct SahBuilder {
       mid = int(it - r.begin());
       // leaf if splitting does not pay (SAH with traversal cost 1, isect cost 1)
       double parent_area = bx_area(bn[id].b);
-      if (cnt <= 4 && parent_area > 0 && 1.0 + best_cost / parent_area >= (double)cnt) {
+      if (cnt <= kLeafSplit && parent_area > 0 && kTrav + best_cost / parent_area >= (double)cnt) {
         bn[id].first = st;
         bn[id].count = cnt;
         return id;
@@ -248,6 +271,7 @@ struct SahBuilder {
       return;
     }
     bn.clear();
+    set_leaf_rules(r.size());
     int root = build(r, 0, (int)r.size(), 0);
     H.bvh_depth = max_depth_seen;
     // store the items in leaf order: a leaf is a contiguous item range
