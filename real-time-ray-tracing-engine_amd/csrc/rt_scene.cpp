@@ -127,11 +127,14 @@ struct SahBuilder {
   // RT_SAH_LEAF_MAX, RT_SAH_LEAF_SPLIT, RT_SAH_TRAV_X4 (4 x trav_cost).
   int leaf_max = 2, leaf_split = 4;
   double trav_cost = 1.0;
+  static constexpr int kMaxBins = 64;
+  int sah_bins = 16; // centroid bins per axis (RT_SAH_BINS: measurement override, <= 64)
   void set_leaf_rules(size_t n_items) {
     const bool binary = n_items < (size_t)kBvh4Min;
     leaf_max = env_int("RT_SAH_LEAF_MAX", binary ? 1 : 2);
     leaf_split = env_int("RT_SAH_LEAF_SPLIT", binary ? 1 : 4);
     trav_cost = env_int("RT_SAH_TRAV_X4", 4) / 4.0;
+    sah_bins = std::min(kMaxBins, std::max(2, env_int("RT_SAH_BINS", 16)));
   }
 
   int build(std::vector<BRef> &r, int st, int en, int dep) {
@@ -165,13 +168,13 @@ struct SahBuilder {
     bool force_median = dep + need >= RT_STACK_DEPTH - 2;
     int best_axis = -1, best_bin = -1;
     double best_cost = kInf;
-    const int kBins = 16;
+    const int kBins = sah_bins;
     if (!force_median) {
       for (int ax = 0; ax < 3; ++ax) {
         double lo = cb.lo[ax], hi = cb.hi[ax];
         if (!(hi - lo > 1e-12)) continue;
-        Bx bb[kBins];
-        int bc[kBins];
+        Bx bb[kMaxBins];
+        int bc[kMaxBins];
         for (int k = 0; k < kBins; ++k) {
           bb[k] = bx_empty();
           bc[k] = 0;
@@ -182,8 +185,8 @@ struct SahBuilder {
           bb[k] = bx_join(bb[k], r[i].b);
           bc[k]++;
         }
-        Bx lb[kBins];
-        int lc[kBins];
+        Bx lb[kMaxBins];
+        int lc[kMaxBins];
         Bx acc = bx_empty();
         int a = 0;
         for (int k = 0; k < kBins; ++k) {
