@@ -42,7 +42,10 @@ using namespace rtp;
 #ifndef RT_REGEN_FLAT
 #define RT_REGEN_FLAT 16
 #endif
-#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? 16 : 1))
+#ifndef RT_REGEN_PLAIN
+#define RT_REGEN_PLAIN 16
+#endif
+#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? RT_REGEN_PLAIN : 1))
 #endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
