@@ -74,6 +74,9 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #ifndef RT_UNIT_PREFETCH
 #define RT_UNIT_PREFETCH 0
 #endif
+#ifndef RT_KARG_FRESH
+#define RT_KARG_FRESH 1
+#endif
 #ifndef RT_PERSIST_FLAT
 #define RT_PERSIST_FLAT 0
 #endif
@@ -81,6 +84,60 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0 || (RT_PERSIST_FLAT && (F) == F_FLAT))
 #endif
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
+
+// The launch fields read afresh from the kernarg segment at each work unit
+// (FRESH, the persistent instances): the asm hides the segment pointer's
+// value, so the loads stay inside the unit loop instead of being hoisted out
+// of it and held in SGPRs across every path trip.  KArgs mirrors
+// render_tiles' explicit arguments (laid out in order, naturally aligned);
+// the parameter's own address is never taken (that copies it to scratch).
+struct KArgs {
+  DScene S;
+  DCamera C;
+  DLaunch P;
+  double *out;
+  unsigned long long *stats;
+};
+template <bool FRESH>
+__device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
+  if constexpr (FRESH) {
+    auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const __attribute__((address_space(4))) DLaunch &K = ka->P;
+    DLaunch L;
+    L.row_begin = K.row_begin;
+    L.row_end = K.row_end;
+    L.sample_begin = K.sample_begin;
+    L.sample_count = K.sample_count;
+    L.seed_lo = K.seed_lo;
+    L.seed_hi = K.seed_hi;
+    L.output = K.output;
+    L.accumulate = K.accumulate;
+    L.tiles_x = K.tiles_x;
+    L.tiles_y = K.tiles_y;
+    L.tile_first = K.tile_first;
+    L.tile_stride = K.tile_stride;
+    L.n_local_tiles = K.n_local_tiles;
+    L.compact = K.compact;
+    L.n_chunks = K.n_chunks;
+    L.chunk_strata = K.chunk_strata;
+    L.unit_ctr = K.unit_ctr;
+    L.grid_cap = K.grid_cap;
+    return L;
+  } else {
+    return P;
+  }
+}
+template <bool FRESH>
+__device__ __forceinline__ double *out_arg(double *out) {
+  if constexpr (FRESH) {
+    auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    return ka->out;
+  } else {
+    return out;
+  }
+}
 
 // PC ("persistent, chunked"): the instance for frame launches split into
 // stratum chunks (rtk_launch_render_chunked: tiles 0.., compact partials, plain
@@ -128,12 +185,13 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   if (PC && P.unit_ctr != nullptr && lane == 0)
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
-  const int local_tile = unit / P.n_chunks, chunk = unit - local_tile * P.n_chunks;
-  const int tile = PC ? local_tile : P.tile_first + local_tile * P.tile_stride;
-  const int s_first = P.sample_begin + chunk * P.chunk_strata;
-  const int s_count = min(P.chunk_strata, P.sample_count - chunk * P.chunk_strata);
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const int x0 = tx * 8, y0 = P.row_begin + ty * 8;
+  const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
+  const int local_tile = unit / PU.n_chunks, chunk = unit - local_tile * PU.n_chunks;
+  const int tile = PC ? local_tile : PU.tile_first + local_tile * PU.tile_stride;
+  const int s_first = PU.sample_begin + chunk * PU.chunk_strata;
+  const int s_count = min(PU.chunk_strata, PU.sample_count - chunk * PU.chunk_strata);
+  const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
+  const int x0 = tx * 8, y0 = PU.row_begin + ty * 8;
   acc[lane * 3 + 0] = 0.0;
   acc[lane * 3 + 1] = 0.0;
   acc[lane * 3 + 2] = 0.0;
@@ -200,7 +258,8 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
         sy = C.scale * sy;
         sz = C.scale * sz;
       }
-      double *o = compact ? out + 3 * ((size_t)unit * 64 + lane)
+      double *const ob = out_arg<PC && RT_KARG_FRESH>(out);
+      double *o = compact ? ob + 3 * ((size_t)unit * 64 + lane)
                             : out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
       if (!PC && P.accumulate) {
         o[0] += sx;
