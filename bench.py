@@ -12,14 +12,25 @@ instead and combines full-frame sums with an RCCL reduce(sum).  Strong scaling:
 the frame is fixed, N varies.
 
 Output: ONE JSON line on rank 0 (driver contract) with
-  * a roofline object for the render kernel: bound "valu" (the kernel issues
-    vector instructions most cycles; the scene is cache/LDS-resident), frac =
-    VALU-busy from rocprofv3 PMC passes that bench.py runs on this build and
-    workload before the timed run; physical HBM bytes per launch (traffic) and
-    GB/s, fp64 TFLOP/s, and SURVEY §8(d)'s algorithmic bytes as the
-    cache-served figure beside it;
-  * a CPU baseline: the reference's own StaticCamera::render -p (ThreadPool of
-    hardware_concurrency() workers) on the host cores, bounded sample.
+  * a roofline object for the render kernel: bound "valu" -- the kernel issues
+    vector instructions most cycles and the scene is cache/LDS-resident, so the
+    roof is the fp64 vector peak (78.6 TFLOP/s); achieved = fp64 FLOP per
+    launch (rocprofv3 PMC passes bench.py runs on this build and workload
+    before the timed run) / the live HIP-event kernel time.  VALU-busy, the
+    fp64 share of the VALU instructions, physical HBM bytes per launch
+    (traffic) and GB/s sit beside it, and SURVEY §8(d)'s algorithmic bytes as
+    the cache-served figure;
+  * the other single-GPU BASELINE configs (C3, C4, C5) timed the same way, C3
+    with its own live PMC passes and roofline;
+  * the host-output rate (rt_render: kernel + D2H into caller host memory,
+    pinned and pageable) and the progressive ("real-time") frame rate per
+    scene (one stratum per frame + device to-bytes, with and without the bytes
+    copied to the host every frame);
+  * a CPU baseline: the reference's own render_cpu -p loop on its ThreadPool
+    sized to the CPUs this process may use (the as-shipped pool of
+    hardware_concurrency() workers beside it), bounded sample.
+  * N>1: per-rank kernel ms (min/mean/max over ranks) and rank 0's exchange
+    wait, measured in serial diagnostic steps after the timed region.
 """
 import argparse
 import json
@@ -94,10 +105,10 @@ def pmc_counters(path_glob_root, kernel_tag="render_tiles<false"):
     return {k: sums[k] / counts[k] for k in sums}, max(counts.values()) if counts else 0
 
 
-def pmc_live(args):
+def pmc_live(args, config=None):
     """rocprofv3 PMC passes over THIS build and workload, run by bench.py itself
     before it touches the GPU (each pass: a child `bench.py --pmc off` of the
-    same config, 1 warmup + 2 steps; counters averaged over the plain render
+    config, 1 warmup + 2 steps; counters averaged over the plain render
     kernel's launches).  Returns the summary dict or None (no rocprofv3 / a pass
     failed: the caller falls back to the committed profiles/pmc_<config>.json)."""
     import shutil
@@ -107,11 +118,12 @@ def pmc_live(args):
     if not prof:
         return None
     tmp = tempfile.mkdtemp(prefix="rtx_pmc_")
-    child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2",
+    config = config or args.config
+    child = [sys.executable, os.path.abspath(__file__), "--config", config, "--steps", "2",
              "--warmup", "1", "--no-cpu-baseline", "--pmc", "off", "--no-other-configs"]
-    if args.width:
+    if config == args.config and args.width:
         child += ["--width", str(args.width)]
-    if args.spp:
+    if config == args.config and args.spp:
         child += ["--spp", str(args.spp)]
     res = {}
     env = dict(os.environ, TMPDIR="/tmp")
@@ -119,7 +131,8 @@ def pmc_live(args):
         d = os.path.join(tmp, name)
         cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc"] + ctrs + [
             "--output-format", "csv", "-d", d, "-o", name, "--"] + child
-        print("bench: PMC pass %s (%s)" % (name, " ".join(ctrs)), file=sys.stderr, flush=True)
+        print("bench: %s PMC pass %s (%s)" % (config, name, " ".join(ctrs)), file=sys.stderr,
+              flush=True)
         try:
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
                                timeout=260)
@@ -147,7 +160,56 @@ def pmc_live(args):
                                     + 128 * res["SQ_INSTS_VALU_FMA_F64"]),
         "valu_busy": round(4 * res["SQ_ACTIVE_INST_VALU"] / (res["GRBM_GUI_ACTIVE"] / 8 * 1024), 4),
         "launches": [res["launches_" + k] for k in PMC_PASSES],
+        "config": config,
     }
+
+
+def load_pmc(args, config, live):
+    """The live PMC summary, else the committed profiles/pmc_<config>.json."""
+    if live is not None:
+        return live
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
+    if args.pmc == "off" or not os.path.exists(path):
+        return None
+    try:
+        pmc = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    pmc["source"] = "committed file profiles/pmc_%s.json (an earlier PMC run)" % config
+    return pmc
+
+
+def roofline(pmc, kernel_ms):
+    """Roofline of the render kernel: the fp64 vector roof (the kernel is
+    VALU-issue bound and LDS/cache resident).  achieved = fp64
+    FLOP per launch (PMC: 64 per ADD/MUL/TRANS, 128 per FMA wave instruction) /
+    the HIP-event kernel time; VALU-busy, the fp64 share of VALU instructions
+    and the physical HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md) per launch beside it."""
+    kernel_s = kernel_ms * 1e-3
+    roof = {"bound": "valu", "unit": "TFLOP/s", "peak": F64_PEAK_TFS, "achieved": None,
+            "frac": None, "traffic": None, "kernel_ms": round(kernel_ms, 3)}
+    if not pmc:
+        return roof
+    if pmc.get("f64_flops_per_launch"):
+        tfs = pmc["f64_flops_per_launch"] / kernel_s / 1e12
+        roof["achieved"] = round(tfs, 3)
+        roof["frac"] = round(tfs / F64_PEAK_TFS, 4)
+    if pmc.get("valu_busy") is not None:
+        roof["valu_busy"] = pmc["valu_busy"]
+    if pmc.get("valu_insts_per_launch") and pmc.get("f64_insts_per_launch"):
+        roof["f64_inst_share"] = round(pmc["f64_insts_per_launch"] / pmc["valu_insts_per_launch"], 4)
+        roof["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]
+        roof["f64_insts_per_launch"] = pmc["f64_insts_per_launch"]
+    if pmc.get("hbm_bytes_per_launch"):
+        tb = pmc["hbm_bytes_per_launch"]
+        roof["traffic"] = tb
+        roof["hbm_read_bytes"] = pmc.get("hbm_read_bytes_per_launch")
+        roof["hbm_write_bytes"] = pmc.get("hbm_write_bytes_per_launch")
+        roof["hbm_gbs"] = round(tb / kernel_s / 1e9, 2)
+        roof["hbm_frac"] = round(tb / kernel_s / 1e9 / HBM_PEAK_GBS, 5)
+    roof["pmc_source"] = pmc.get("source")
+    return roof
 
 
 def host_cpu_info():
@@ -188,29 +250,37 @@ def grow(run, target_s):
 
 
 def cpu_baseline(scene, cam_full):
-    """The reference's OWN multithreaded CPU path: StaticCamera::render with -p
-    (use_parallelism), i.e. render_cpu's ThreadPool of
-    std::thread::hardware_concurrency() workers, one task per pixel, a barrier per
-    row, and its PPM writer (StaticCamera.cpp:32-100, ThreadPool.hpp:6-174),
-    compiled from /root/reference/src into oracle/_ref.
+    """The reference's OWN multithreaded CPU path, compiled from
+    /root/reference/src into oracle/_ref: render_cpu's -p loop (one task per
+    pixel, a barrier per row, StaticCamera.cpp:32-100) on the reference's
+    ThreadPool (ThreadPool.hpp:6-174), with as many workers as CPUs this process
+    may use (the cgroup quota / affinity) -- `value`.  Beside it, as shipped:
+    StaticCamera::render -p with its pool of std::thread::hardware_concurrency()
+    workers and its PPM writer (`as_shipped_*`); on a box whose quota is far
+    below the machine's CPUs its spinning workers oversubscribe the quota.
 
-    Bounded sample: the same scene and depth at 960x540 (the reference pool's
+    Bounded samples: the same scene and depth at 960x540 (the reference pool's
     1024-slot Chase-Lev deque overflows on rows wider than 1023 pixels and
     corrupts the heap -- measured: `malloc(): unaligned fastbin chunk detected`
     at 1920 wide, WorkStealingDeque.hpp:29-43 vs :72-85 -- so the sample keeps
     rows short), at the square sample count grow() reaches from 1 spp for a
-    timed run of ~8-15 s of CPU work."""
+    timed run of ~5-10 s; the as-shipped run at 480x270, 1 spp upwards."""
     import ctypes as C
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     host = host_cpu_info()
-    width = 960
-    h = max(1, int(width / cam_full.aspect_ratio))
+    hw = host["hardware_concurrency"]
+    usable = host.get("cgroup_cpu_quota") or host.get("affinity_cpus") or hw
+    usable = max(1, min(hw, int(usable)))
+    ref = O.ref_available()
 
-    def run(spp):
-        cam = scene.camera_desc(image_width=width, samples_per_pixel=spp,
-                                max_depth=cam_full.max_depth)
+    def cam_at(width, spp):
+        return scene.camera_desc(image_width=width, samples_per_pixel=spp,
+                                 max_depth=cam_full.max_depth)
+
+    def run_static(width, spp):
+        cam = cam_at(width, spp)
         d = scene.desc()
         cwd = os.getcwd()
         tmp = tempfile.mkdtemp(prefix="rtx_cpu_")
@@ -220,11 +290,11 @@ def cpu_baseline(scene, cam_full):
             with open(os.path.join(tmp, "clog.txt"), "w") as f:
                 os.dup2(f.fileno(), 2)  # its "Scanlines remaining" progress (std::clog)
                 t = time.perf_counter()
-                if O.ref_available():
+                if ref:
                     O.ref().ref_render_static(C.byref(d), C.byref(cam), 1, int(scene.use_bvh), 1,
                                               b"cpu_baseline.ppm")
                 else:  # reference build absent: the oracle restatement, same decomposition
-                    O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=host["hardware_concurrency"])
+                    O.oracle_render(scene, cam, O.MODE_COUNTER, 1, threads=usable)
                 dt = time.perf_counter() - t
         finally:
             os.dup2(err, 2)
@@ -232,35 +302,40 @@ def cpu_baseline(scene, cam_full):
             os.chdir(cwd)
         return dt
 
-    spp, dt = grow(run, 15.0)
-    n = width * h * spp
-    out = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s",
-           "cores": host["hardware_concurrency"],
-           "kind": "reference" if O.ref_available() else "port",
-           "sample": "StaticCamera::render -p (ThreadPool, hardware_concurrency() = %d workers), "
-                     "%s %dx%d @ %d spp, depth %d, %.1f s" % (
-                         host["hardware_concurrency"], scene_name_of(scene), width, h, spp,
-                         cam_full.max_depth, dt)}
-    out.update({k: v for k, v in host.items() if k != "hardware_concurrency"})
-    # The box may cap this process below hardware_concurrency() (cgroup CPU
-    # quota): the reference's pool then oversubscribes the quota with spinning
-    # workers.  Beside the primary figure, the same -p loop on the reference's
-    # ThreadPool sized to the quota.
-    quota = host.get("cgroup_cpu_quota") or host.get("affinity_cpus")
-    if O.ref_available() and quota and int(quota) < host["hardware_concurrency"]:
-        nt = max(1, int(quota))
+    def hgt(width):
+        return max(1, int(width / cam_full.aspect_ratio))
+
+    name = scene_name_of(scene)
+    out = {"unit": "Msamples/s", "kind": "reference" if ref else "port"}
+    if ref:
+        width = 960
 
         def run_pool(spp):
-            cam = scene.camera_desc(image_width=width, samples_per_pixel=spp,
-                                    max_depth=cam_full.max_depth)
             t = time.perf_counter()
-            O.ref_trace_pool(scene, cam, nt)
+            O.ref_trace_pool(scene, cam_at(width, spp), usable)
             return time.perf_counter() - t
-        spp2, dt2 = grow(run_pool, 10.0)
-        out["quota_sized_pool"] = {
-            "value": round(width * h * spp2 / dt2 / 1e6, 4), "unit": "Msamples/s", "cores": nt,
-            "sample": "render_cpu -p loop on the reference ThreadPool with %d workers, "
-                      "%dx%d @ %d spp, %.1f s" % (nt, width, h, spp2, dt2)}
+        spp, dt = grow(run_pool, 10.0)
+        out.update({"value": round(width * hgt(width) * spp / dt / 1e6, 4), "cores": usable,
+                    "sample": "render_cpu -p loop on the reference ThreadPool with %d workers "
+                              "(the CPUs this process may use), %s %dx%d @ %d spp, depth %d, "
+                              "%.1f s" % (usable, name, width, hgt(width), spp,
+                                          cam_full.max_depth, dt)})
+        w2 = 480 if usable < hw else 960
+        spp2, dt2 = grow(lambda n: run_static(w2, n), 6.0)
+        out.update({"as_shipped_value": round(w2 * hgt(w2) * spp2 / dt2 / 1e6, 4),
+                    "as_shipped_workers": hw,
+                    "as_shipped_sample": "StaticCamera::render -p (ThreadPool of "
+                                         "hardware_concurrency() = %d workers, PPM writer), "
+                                         "%s %dx%d @ %d spp, %.1f s" % (
+                                             hw, name, w2, hgt(w2), spp2, dt2)})
+    else:
+        width = 960
+        spp, dt = grow(lambda n: run_static(width, n), 10.0)
+        out.update({"value": round(width * hgt(width) * spp / dt / 1e6, 4), "cores": usable,
+                    "sample": "oracle restatement (reference build absent), %d threads, "
+                              "%s %dx%d @ %d spp, %.1f s" % (usable, name, width, hgt(width),
+                                                             spp, dt)})
+    out.update({k: v for k, v in host.items()})
     return out
 
 
@@ -268,27 +343,31 @@ def scene_name_of(scene):
     return getattr(scene, "_name", "scene")
 
 
-def other_configs(args, torch, dev, skip):
-    """The other single-GPU BASELINE configs at their full size (C3: 486-sphere BVH
-    scene at spp 256; C4: Cornell + fog + Perlin at spp 1024), timed like the
-    headline (device-resident frame buffer, barrier-free single rank, K steps
-    bracketed by device syncs) so the bench line carries every 1080p config."""
+def other_configs(args, torch, dev, skip, pmcs):
+    """The other single-GPU BASELINE configs at their full size (C3: 486-sphere
+    BVH scene at spp 256; C4: Cornell + fog + Perlin at spp 1024; C5: the
+    486-sphere scene with motion blur at 3840x2160, spp 4096 -- BASELINE names
+    it an 8-GPU config; one GPU renders the whole frame here), timed like the
+    headline (device-resident frame buffer, single rank, K steps bracketed by
+    device syncs, HIP-event kernel time), so the bench line carries every
+    config; C3 also with its own roofline (live PMC passes when available)."""
     from rtx import abi
     from rtx.render import Renderer, camera_frame
     from rtx.scene import load_scene
     res = {}
-    for c in ("C3", "C4"):
+    plan = {"C3": (1, 4), "C4": (1, 2), "C5": (1, 1)}  # (warmup, steps)
+    for c, (warm, steps) in plan.items():
         if c == skip:
             continue
         name, width, spp, depth = CONFIGS[c]
         S = load_scene(os.path.join(SCENES, name + ".json"))
         f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
         buf = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
-        steps = 2 if c == "C4" else 4
         with Renderer(S, device=dev.index or 0) as R:
             def go(seed):
                 R.render_device(f, buf.data_ptr(), 0, seed=seed, output=abi.RT_OUT_SUM, accumulate=0)
-            go(999)
+            for w in range(warm):
+                go(999 + w)
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             ms = []
@@ -297,13 +376,138 @@ def other_configs(args, torch, dev, skip):
                 ms.append(R.last_kernel_ms())
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
+            finite = bool(torch.isfinite(buf).all().item())
         n = f.image_width * f.image_height * f.sqrt_spp ** 2 * steps
+        kms = sum(ms) / len(ms)
         res[c] = {"workload": "%s %s %dx%d spp%d depth%d" % (c, name, f.image_width, f.image_height,
                                                              f.sqrt_spp ** 2, depth),
                   "value": round(n / dt / 1e6, 3), "unit": "Msamples/s", "steps": steps,
-                  "ms_per_step": round(dt * 1e3 / steps, 3),
-                  "kernel_ms": round(sum(ms) / len(ms), 3)}
+                  "warmup": warm, "ms_per_step": round(dt * 1e3 / steps, 3),
+                  "kernel_ms": round(kms, 3), "finite": finite}
+        if c in pmcs:
+            res[c]["roofline"] = roofline(pmcs[c], kms)
     return res
+
+
+def host_output(torch, R, frame, steps):
+    """rt_render, the drop-in for render_gpu's batch loop: the frame kernel plus
+    the D2H copy of the scaled radiance into caller host memory, synchronous.
+    Pinned (page-locked) and pageable caller buffers."""
+    import numpy as np
+    n = frame.image_width * frame.image_height * frame.sqrt_spp ** 2
+    res = {}
+    pinned = torch.empty((frame.image_height, frame.image_width, 3), dtype=torch.float64,
+                         pin_memory=True)
+    pageable = np.empty((frame.image_height, frame.image_width, 3), dtype=np.float64)
+    for kind, ptr in (("pinned", pinned.data_ptr()), ("pageable", pageable.ctypes.data)):
+        R.render_into(frame, ptr, seed=77)  # warm (first touch of the pages)
+        t0 = time.perf_counter()
+        kms = []
+        for k in range(steps):
+            R.render_into(frame, ptr, seed=k)
+            kms.append(R.last_kernel_ms())
+        dt = (time.perf_counter() - t0) / steps
+        res[kind] = {"value": round(n / dt / 1e6, 3), "unit": "Msamples/s",
+                     "ms_per_step": round(dt * 1e3, 3),
+                     "kernel_ms": round(sum(kms) / len(kms), 3),
+                     "copy_ms": round(dt * 1e3 - sum(kms) / len(kms), 3),
+                     "bytes_per_step": frame.image_width * frame.image_height * 24}
+    res["note"] = ("rt_render: render + D2H of the %d MB fp64 frame into caller memory, "
+                   "host-synchronous per frame" % (frame.image_width * frame.image_height * 24 // 10 ** 6))
+    return res
+
+
+def progressive_rates(torch, dev, width=1920, frames=30):
+    """The real-time half (DynamicCamera.cpp:350-564): one
+    stratum of every pixel per frame, added into a device accumulator
+    (rt_render_device, accumulate) and quantised on the device
+    (rt_to_bytes_device), on the null stream.  Per scene at 1080p:
+      device_ms  -- frames issued back to back, one sync at the end;
+      display_ms -- every frame also copies its 6.2 MB of bytes to pinned host
+                    memory and waits for them (what a viewer must do per frame;
+                    the reference copies the whole 49.8 MB fp64 accumulator back,
+                    DynamicCamera.cpp:524-532)."""
+    from rtx.progressive import for_renderer, frame_bytes
+    from rtx.render import Renderer, camera_frame
+    from rtx.scene import load_scene
+    res = {}
+    for c in ("C2", "C3", "C4"):
+        name, _, spp, depth = CONFIGS[c]
+        S = load_scene(os.path.join(SCENES, name + ".json"))
+        f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
+        with Renderer(S, device=dev.index or 0) as R:
+            pr = for_renderer(R, f, seed=5)
+            out = torch.empty(pr.acc.shape, dtype=torch.uint8, device=dev)
+            host = torch.empty(pr.acc.shape, dtype=torch.uint8, pin_memory=True)
+            for _ in range(2):  # warm
+                pr.step(1)
+                frame_bytes(pr, out)
+            torch.cuda.synchronize(dev)
+            pr.reset()
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                pr.step(1)
+                frame_bytes(pr, out)
+            torch.cuda.synchronize(dev)
+            dev_ms = (time.perf_counter() - t0) * 1e3 / frames
+            pr.reset()
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                pr.step(1)
+                frame_bytes(pr, out)
+                host.copy_(out, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+            disp_ms = (time.perf_counter() - t0) * 1e3 / frames
+        res[c] = {"scene": name, "width": f.image_width, "height": f.image_height,
+                  "strata_per_frame": 1, "frames_to_converge": f.sqrt_spp ** 2,
+                  "device_ms_per_frame": round(dev_ms, 3), "device_fps": round(1e3 / dev_ms, 1),
+                  "display_ms_per_frame": round(disp_ms, 3), "display_fps": round(1e3 / disp_ms, 1)}
+    return res
+
+
+def rank_diagnostics(torch, dist, dev, rank, ws, launch_work, exchange, wait_exchange, steps=2):
+    """N>1: serial diagnostic steps after the timed region.  Each step: barrier,
+    this rank's render timed with HIP events on its launch stream, then the
+    frame exchange timed on the host from this rank's render completion to the
+    exchange's completion (rank 0: the wait for the slowest rank plus the
+    transfer).  Returns per-rank kernel ms and exchange ms, gathered on every
+    rank (min / mean / max, and the per-rank lists)."""
+    cuda = dev.type == "cuda"  # the CPU tests drive the same code with host clocks
+    stream = torch.cuda.current_stream(dev) if cuda else None
+    kms, xms = [], []
+    for k in range(steps):
+        dist.barrier()
+        if cuda:
+            torch.cuda.synchronize(dev)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            launch_work(6000 + k, 0)
+            e1.record(stream)
+            e1.synchronize()
+            kms.append(e0.elapsed_time(e1))
+        else:
+            t0 = time.perf_counter()
+            launch_work(6000 + k, 0)
+            kms.append((time.perf_counter() - t0) * 1e3)
+        t0 = time.perf_counter()
+        wait_exchange(exchange(0))
+        if cuda:
+            torch.cuda.synchronize(dev)
+        xms.append((time.perf_counter() - t0) * 1e3)
+    mine = torch.tensor([sum(kms) / len(kms), sum(xms) / len(xms)], dtype=torch.float64)
+    if dist.get_backend() == "nccl" and cuda:
+        mine = mine.to(dev)
+    allv = [torch.zeros_like(mine) for _ in range(ws)]
+    dist.all_gather(allv, mine)
+    per_k = [round(float(v[0]), 3) for v in allv]
+    per_x = [round(float(v[1]), 3) for v in allv]
+    return {"kernel_ms_min": min(per_k), "kernel_ms_mean": round(sum(per_k) / ws, 3),
+            "kernel_ms_max": max(per_k), "exchange_ms_rank0": per_x[0],
+            "exchange_ms_max": max(per_x), "per_rank_kernel_ms": per_k,
+            "per_rank_exchange_ms": per_x, "diagnostic_steps": steps,
+            "note": "serial steps after the timed region: render (HIP events), then the "
+                    "exchange from this rank's render end to its completion (host clock)"}
 
 
 def main():
@@ -342,11 +546,17 @@ def main():
 
     ws, rank, local = dist_env()
     pmc = None
+    full_line = ws == 1 and not args.no_other_configs and not args.width and not args.spp
+    pmc_other = {}
     if ws == 1 and args.pmc == "auto":  # before this process initialises the GPU
         pmc = pmc_live(args)
         if pmc and args.pmc_save:
             with open(args.pmc_save, "w") as fh:
                 json.dump(dict(pmc, config=args.config), fh, indent=1)
+        if full_line and args.config != "C3":
+            pmc_other["C3"] = pmc_live(args, "C3")
+    if full_line and args.config != "C3":
+        pmc_other["C3"] = load_pmc(args, "C3", pmc_other.get("C3"))
     import torch
     from rtx import abi
     from rtx.render import Renderer, camera_frame
@@ -480,10 +690,13 @@ def main():
         scale = max(1.0, ref.abs().max().item())
         check = {"max_abs_diff": err, "ok": bool(err <= 1e-9 * scale)}
 
+    diag = None
     if ws > 1:  # kernel time measured after the timed region (no sync inside it)
         for k in range(min(2, args.steps)):
             launch_work(5000 + k, 0)
             kernel_ms.append(R.last_kernel_ms())
+        diag = rank_diagnostics(torch, dist, dev, rank, ws, launch_work, exchange,
+                                lambda w: w.wait() if w is not None else None)
 
     samples_per_step = W * H * n_strata  # whole frame, all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
@@ -498,41 +711,8 @@ def main():
     bytes_launch = algorithmic_bytes(st, info, px_launch)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if pmc is None and ws == 1 and args.pmc != "off" and os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            pmc["source"] = "committed file profiles/pmc_%s.json (an earlier PMC run)" % args.config
-        except (OSError, ValueError):
-            pmc = None
-    kernel_s = avg_ms * 1e-3
-    # The binding roof is vector-ALU issue: the scene is
-    # L1/L2/LDS-resident, so HBM carries only the accumulator.  frac = VALU-busy,
-    # SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (GRBM_GUI_ACTIVE / 8 XCDs x 1024
-    # SIMDs), from the PMC passes; physical HBM traffic (FETCH_SIZE x 2 +
-    # WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) is reported beside it.
-    roof = {"bound": "valu", "unit": "fraction of SIMD cycles issuing VALU", "peak": 1.0,
-            "achieved": None, "frac": None, "traffic": None, "kernel_ms": round(avg_ms, 3)}
-    if pmc and pmc.get("valu_busy") is not None:
-        roof["achieved"] = roof["frac"] = pmc["valu_busy"]
-    if pmc and pmc.get("hbm_bytes_per_launch"):
-        tb = pmc["hbm_bytes_per_launch"]
-        roof["traffic"] = tb
-        roof["hbm"] = {"bytes_per_launch": tb, "read_bytes_per_launch": pmc.get("hbm_read_bytes_per_launch"),
-                       "write_bytes_per_launch": pmc.get("hbm_write_bytes_per_launch"),
-                       "achieved_gbs": round(tb / kernel_s / 1e9, 2), "peak_gbs": HBM_PEAK_GBS,
-                       "frac": round(tb / kernel_s / 1e9 / HBM_PEAK_GBS, 5)}
-    if pmc and pmc.get("f64_flops_per_launch"):
-        tfs = pmc["f64_flops_per_launch"] / kernel_s / 1e12
-        roof["f64"] = {"achieved_tflops": round(tfs, 3), "peak_tflops": F64_PEAK_TFS,
-                       "frac": round(tfs / F64_PEAK_TFS, 4),
-                       "valu_insts_per_launch": pmc.get("valu_insts_per_launch"),
-                       "f64_insts_per_launch": pmc.get("f64_insts_per_launch")}
-    if pmc:
-        roof["pmc_source"] = pmc.get("source")
-    # SURVEY §8(d)'s algorithmic bytes: what the traversal/shading reads from the
-    # scene tables per launch.  Served by LDS/L1/L2, not HBM -- a cache-side
-    # figure, never an HBM fraction.
+    pmc = load_pmc(args, args.config, pmc) if ws == 1 else None
+    roof = roofline(pmc, avg_ms)
     roof["cache_served"] = {"bytes_per_launch": int(bytes_launch),
                             "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
                             "gbs": round(achieved, 1)}
@@ -546,7 +726,8 @@ def main():
         "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
         "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
         "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
-    roof["note"] = ("VALU-issue bound; N>1 lines carry no PMC data (traffic null)"
+    roof["note"] = ("fp64 vector roof (VALU-issue bound, scene LDS/cache resident); "
+                    "N>1 lines carry no PMC data (traffic null)"
                     if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")
 
     out = {
@@ -576,8 +757,13 @@ def main():
     }
     if check is not None:
         out["check"] = check
-    if rank == 0 and ws == 1 and not args.no_other_configs and not args.width and not args.spp:
-        out["other_configs"] = other_configs(args, torch, dev, args.config)
+    if diag is not None:
+        out["ranks"] = diag
+    if rank == 0 and full_line:
+        out["other_configs"] = other_configs(args, torch, dev, args.config, pmc_other)
+        if not tiles_mode:
+            out["host_output"] = host_output(torch, R, frame, max(3, min(args.steps, 10)))
+        out["progressive"] = progressive_rates(torch, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, cam)
     if rank == 0:

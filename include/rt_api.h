@@ -57,7 +57,13 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+/* Bumped whenever a struct layout or a signature below changes.  A caller
+   checks rt_abi_version() == the RT_ABI_VERSION it was compiled against before
+   any other call (rtx/lib.py does): structs are passed by pointer without a
+   size field, so a caller built against another version must not proceed.
+   2: rt_scene_desc.bvh_arity, rt_path_stats.cyc_*, rt_scene_info's stack and
+      LDS fields. */
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define RT_OK 0
@@ -286,6 +292,12 @@ typedef struct rt_scene_info {
   int32_t bvh_builder;  /* the builder that made the world BVH: RT_BVH_HOST / RT_BVH_DEVICE /
                            RT_BVH_DEVICE_SAH */
   int32_t bvh_arity;    /* 2 or 4 (n_nodes, lds_nodes and node_bytes count nodes of this width) */
+  int32_t stack_depth;  /* traversal stack entries per lane (1 + BVH levels; 3 per 4-wide level) */
+  int32_t lds_fixed_bytes;  /* LDS per block the kernel needs before staging nodes: static
+                               accumulators + traversal stacks of its 4 wavefronts */
+  int32_t lds_block_budget; /* LDS per block at the kernel's occupancy target; the node prefix
+                               fills what lds_fixed_bytes leaves (LDS never lowers occupancy) */
+  int32_t waves_per_simd;   /* occupancy target of the kernel instance the scene selects */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */
@@ -339,8 +351,11 @@ int rt_to_bytes_device(const double *device_rgb, int64_t n_pixels, double scale,
 typedef struct rt_multi rt_multi; /* opaque: one rt_scene per shard */
 
 /* One scene per shard, shard k on devices[k % n_devices] (n_shards may exceed
-   n_devices: virtual shards share a device).  The scenes are compiled and
-   uploaded by one host thread per shard. */
+   n_devices: virtual shards share a device; at most RT_MULTI_MAX_SHARDS, since
+   each shard holds a device copy of the scene and a host thread).  The scenes
+   are compiled and uploaded by one host thread per shard; a failure to start
+   one returns RT_ERR_DEVICE (nothing is thrown across the ABI). */
+#define RT_MULTI_MAX_SHARDS 256
 int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
                     int32_t n_shards, rt_multi **multi);
 

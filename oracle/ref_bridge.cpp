@@ -416,9 +416,32 @@ int ref_object_hit(const rt_scene_desc *d, int obj, const double ray[7], double 
     if (g.mat[k] && g.mat[k] == rec.material) mi = k;
   // ConstantMedium::hit never writes u, v (ConstantMedium.cpp:25-94): whatever
   // the caller's -- or a HittableList's uninitialised temp -- record held stays.
-  // Store 0 for medium hits so the fixtures regenerate byte for byte.
-  for (int k = 0; k < d->n_objects; ++k)
-    if (d->objects[k].kind == RT_OBJ_MEDIUM && d->objects[k].phase == mi) rec.u = rec.v = 0.0;
+  // Store 0 for medium hits so the fixtures regenerate byte for byte.  A hit is
+  // a medium's when its material is the phase material of a medium reachable
+  // from `obj` (through lists and transforms, not into medium boundaries) and
+  // no surface reachable that way carries the same material: a surface's own
+  // u, v are never overwritten.
+  {
+    std::vector<int> todo{obj}, seen(d->n_objects, 0);
+    bool medium_mat = false, surface_mat = false;
+    while (!todo.empty()) {
+      const int k = todo.back();
+      todo.pop_back();
+      if (k < 0 || k >= d->n_objects || seen[k]) continue;
+      seen[k] = 1;
+      const rt_object_desc &o = d->objects[k];
+      if (o.kind == RT_OBJ_MEDIUM) {
+        if (o.phase == mi) medium_mat = true;
+      } else if (o.kind == RT_OBJ_SPHERE || o.kind == RT_OBJ_QUAD) {
+        if (o.material == mi) surface_mat = true;
+      } else if (o.kind == RT_OBJ_LIST) {
+        for (int c = 0; c < o.count; ++c) todo.push_back(d->children[o.child + c]);
+      } else {
+        todo.push_back(o.child); // rotate_y / translate
+      }
+    }
+    if (medium_mat && !surface_mat) rec.u = rec.v = 0.0;
+  }
   double v[12] = {rec.t,        rec.point.x(),  rec.point.y(),  rec.point.z(),
                   rec.normal.x(), rec.normal.y(), rec.normal.z(), rec.u,
                   rec.v,        rec.frontFace ? 1.0 : 0.0, (double)mi, 0};

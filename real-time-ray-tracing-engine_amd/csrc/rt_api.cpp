@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -24,8 +25,7 @@
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
-extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
-                                      int *waves_per_simd);
+extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
 extern "C" size_t rtk_sah_temp_bytes(int n);
 extern "C" hipError_t rtk_build_sah(const double *boxes, const DItem *items_in, int n,
@@ -325,11 +325,18 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   }
   auto P = [&](size_t i) { return (const void *)(s->block + parts[i].off); };
   // with H.nodes holding the final binary tree: collapse and upload the 4-wide
-  // one (kept binary when its stack would not fit RT_STACK_DEPTH4)
-  auto collapse4 = [&]() -> hipError_t {
+  // one -- kept binary when its stack would not fit RT_STACK_DEPTH4, or when
+  // its traversal stacks (three entries per 4-wide level, so a deep or lopsided
+  // collapse costs more LDS than the binary walk's one per level) would not fit
+  // the 4-wide instance's per-block LDS share at its occupancy target: LDS must
+  // never lower occupancy
+  auto collapse4 = [&](int features) -> hipError_t {
     if (!want4 || H.root_is_leaf || H.nodes.empty()) return hipSuccess;
     const int d4 = rtx::collapse_bvh4(H.nodes, H.nodes4);
-    if (rtx::bvh4_stack_depth(d4) > RT_STACK_DEPTH4) {
+    RtkLdsPlan plan4{};
+    hipError_t fe = rtk_lds_plan(features | RT_FEAT_BVH4, rtx::bvh4_stack_depth(d4), &plan4);
+    if (fe != hipSuccess) return fe;
+    if (rtx::bvh4_stack_depth(d4) > RT_STACK_DEPTH4 || !plan4.stack_fits) {
       H.nodes4.clear();
       return hipSuccess;
     }
@@ -414,7 +421,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     d.root_is_leaf = H.root_is_leaf;
     d.n_root_items = H.n_root_items;
   }
-  if ((e = collapse4()) != hipSuccess) {
+  if ((e = collapse4(d.features)) != hipSuccess) {
     rt_scene_destroy(s);
     return hip_err(e, "4-wide BVH upload");
   }
@@ -429,15 +436,21 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     d.n_nodes = (int32_t)H.nodes4.size();
     d.stack_depth = rtx::bvh4_stack_depth(H.bvh_depth4);
   }
+  RtkLdsPlan plan{};
   {
-    int budget = 0, wps = 1, cus = 0;
-    hipError_t be = rtk_node_budget(d.features, d.stack_depth, &budget, &wps);
+    int cus = 0;
+    hipError_t be = rtk_lds_plan(d.features, d.stack_depth, &plan);
     if (be == hipSuccess) be = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    s->wave_slots = cus * 4 * wps;
     if (be != hipSuccess) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
     }
+    if (!plan.stack_fits) { // the binary stack (<= RT_STACK_DEPTH entries) fits the smallest share
+      rt_scene_destroy(s);
+      return set_err(RT_ERR_UNSUPPORTED, "BVH traversal stacks exceed the per-block LDS budget");
+    }
+    s->wave_slots = cus * 4 * plan.waves_per_simd;
+    int budget = plan.n_nodes;
     if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
   }
@@ -461,6 +474,10 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.lds_nodes = d.n_lds_nodes;
   in.bvh_builder = builder;
   in.bvh_arity = H.bvh_arity;
+  in.stack_depth = d.stack_depth;
+  in.lds_fixed_bytes = plan.fixed_bytes;
+  in.lds_block_budget = plan.block_budget;
+  in.waves_per_simd = plan.waves_per_simd;
   *out = s;
   return RT_OK;
 }
@@ -700,19 +717,33 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
   *out = nullptr;
   if (n_devices < 1 || n_shards < n_devices)
     return set_err(RT_ERR_INVALID, "need n_devices >= 1 and n_shards >= n_devices");
-  rt_multi *m = new rt_multi();
-  m->scenes.assign(n_shards, nullptr);
-  m->parts.resize(n_shards);
-  m->ms.assign(n_shards, 0.0);
+  if (n_shards > RT_MULTI_MAX_SHARDS) // each shard holds a device scene copy and a host thread
+    return set_err(RT_ERR_INVALID, "n_shards exceeds RT_MULTI_MAX_SHARDS");
+  rt_multi *m = new (std::nothrow) rt_multi();
+  if (!m) return set_err(RT_ERR_OOM, "host allocation");
   std::vector<int> rc(n_shards, RT_OK);
   std::vector<std::string> err(n_shards);
-  std::vector<std::thread> th;
-  for (int k = 0; k < n_shards; ++k)
-    th.emplace_back([&, k]() {
-      rc[k] = rt_scene_create(desc, devices[k % n_devices], &m->scenes[k]);
-      if (rc[k] != RT_OK) err[k] = g_err; // thread-local message of this worker
-    });
-  for (auto &t : th) t.join();
+  try {
+    m->scenes.assign(n_shards, nullptr);
+    m->parts.resize(n_shards);
+    m->ms.assign(n_shards, 0.0);
+    std::vector<std::thread> th;
+    try {
+      for (int k = 0; k < n_shards; ++k)
+        th.emplace_back([&, k]() {
+          rc[k] = rt_scene_create(desc, devices[k % n_devices], &m->scenes[k]);
+          if (rc[k] != RT_OK) err[k] = g_err; // thread-local message of this worker
+        });
+    } catch (const std::exception &ex) { // thread creation failed: join the started ones
+      for (auto &t : th) t.join();
+      rt_multi_destroy(m);
+      return set_err(RT_ERR_DEVICE, std::string("shard thread: ") + ex.what());
+    }
+    for (auto &t : th) t.join();
+  } catch (const std::exception &ex) { // host allocation inside the containers
+    rt_multi_destroy(m);
+    return set_err(RT_ERR_OOM, std::string("rt_multi_create: ") + ex.what());
+  }
   for (int k = 0; k < n_shards; ++k)
     if (rc[k] != RT_OK) {
       rt_multi_destroy(m);
@@ -743,6 +774,7 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   std::vector<int> src(n, RT_OK);
   std::vector<std::string> err(n);
   std::vector<std::thread> th;
+  try {
   for (int k = 0; k < n; ++k) {
     m->ms[k] = 0.0;
     if (k >= n_tiles) continue; // more shards than tiles
@@ -755,11 +787,21 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
       q.output = RT_OUT_SUM;
       q.accumulate = 0;
       const int64_t local = (n_tiles - k + n - 1) / n;
-      m->parts[k].resize((size_t)local * chunks * 64 * 3);
+      try {
+        m->parts[k].resize((size_t)local * chunks * 64 * 3);
+      } catch (const std::exception &) {
+        src[k] = RT_ERR_OOM;
+        err[k] = "host tile buffer";
+        return;
+      }
       src[k] = rt_render(m->scenes[k], f, &q, m->parts[k].data());
       if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
       if (src[k] != RT_OK) err[k] = g_err;
     });
+  }
+  } catch (const std::exception &ex) { // thread creation failed: join the started ones
+    for (auto &t : th) t.join();
+    return set_err(RT_ERR_DEVICE, std::string("shard thread: ") + ex.what());
   }
   for (auto &t : th) t.join();
   for (int k = 0; k < n; ++k)

@@ -27,6 +27,7 @@
 // -ffp-contract=off so expression rounding follows the reference's order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <array>
 #include <utility>
@@ -98,6 +99,22 @@ struct KArgs {
   double *out;
   unsigned long long *stats;
 };
+// The AMDGPU kernarg segment places explicit arguments in order at their
+// natural alignment -- the layout of this struct.  The expected offsets are
+// spelled out so a field added to DScene / DCamera / DLaunch breaks the build
+// here instead of silently shifting what the persistent instance reads (its
+// frames are also checked bit for bit against the one-unit-per-wave instance
+// on the GPU: tests/test_persistent.py, and through every BASELINE band).
+static_assert(sizeof(DScene) == 144 && alignof(DScene) == 8, "DScene kernarg layout");
+static_assert(sizeof(DCamera) == 208 && alignof(DCamera) == 8, "DCamera kernarg layout");
+static_assert(sizeof(DLaunch) == 80 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
+static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 144 && offsetof(KArgs, P) == 352 &&
+                  offsetof(KArgs, out) == 432 && offsetof(KArgs, stats) == 440 &&
+                  sizeof(KArgs) == 448,
+              "KArgs must mirror render_tiles' kernarg layout");
+static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
+                  offsetof(DLaunch, grid_cap) == 72,
+              "DLaunch field offsets read from the kernarg segment");
 template <bool FRESH>
 __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
   if constexpr (FRESH) {
@@ -358,10 +375,12 @@ extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) 
   return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
 
-// LDS bytes per block left for the staged BVH prefix at the occupancy the
-// instance's register count allows (blocks of kWaves waves over the 4 SIMDs).
-extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_nodes,
-                                      int *waves_per_simd_out) {
+// LDS plan per block at the occupancy the instance's register count allows
+// (blocks of kWaves waves over the 4 SIMDs): the bytes left for the staged BVH
+// prefix after the static LDS and the traversal stacks, and whether those two
+// fit at all (the caller then keeps a shallower tree).  RTX_LDS_CAP lowers the
+// per-block cap (tests of that fallback).
+extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan) {
   hipFuncAttributes a;
   hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(render_table(false)[features & F_ALL]));
   if (e != hipSuccess) return e;
@@ -369,14 +388,19 @@ extern "C" hipError_t rtk_node_budget(int features, int stack_depth, int *n_node
   int waves_per_simd = regs > 0 ? 512 / regs : 8;
   if (waves_per_simd > 8) waves_per_simd = 8;
   if (waves_per_simd < 1) waves_per_simd = 1;
-  *waves_per_simd_out = waves_per_simd;
-  const size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
+  size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
+  if (const char *c = getenv("RTX_LDS_CAP"))
+    if (atoi(c) > 0 && (size_t)atoi(c) < cap) cap = (size_t)atoi(c);
   const int blocks_per_cu = waves_per_simd * 4 / kWaves > 0 ? waves_per_simd * 4 / kWaves : 1;
   size_t per_block = lds_cu / blocks_per_cu;
   if (per_block > cap) per_block = cap;
-  size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(features, stack_depth, 0);
+  const size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(features, stack_depth, 0);
   const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
-  *n_nodes = per_block > fixed ? (int)((per_block - fixed) / node) : 0;
+  plan->waves_per_simd = waves_per_simd;
+  plan->block_budget = (int32_t)per_block;
+  plan->fixed_bytes = (int32_t)fixed;
+  plan->stack_fits = fixed <= per_block;
+  plan->n_nodes = per_block > fixed ? (int)((per_block - fixed) / node) : 0;
   return hipSuccess;
 }
 

@@ -174,6 +174,16 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_FLAT 16  // flat world (root_is_leaf): no BVH walk
 #define RT_FEAT_BVH4 32  // the world BVH is 4-wide (DNode4); never with RT_FEAT_FLAT
 
+// LDS plan of one render instance (rtk_lds_plan): its occupancy target and
+// what the per-block LDS share at that occupancy leaves for staged BVH nodes.
+struct RtkLdsPlan {
+  int32_t waves_per_simd; // resident waves per SIMD the instance's registers allow
+  int32_t block_budget;   // LDS bytes per block at that occupancy (<= 64 KB)
+  int32_t fixed_bytes;    // static LDS + traversal stacks per block
+  int32_t stack_fits;     // fixed_bytes <= block_budget
+  int32_t n_nodes;        // BVH nodes that fit in the rest (BFS prefix)
+};
+
 struct DCamera {     // the rt_frame values the kernel needs
   double center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
   double defocus_angle;

@@ -334,6 +334,11 @@ int main(int argc, char **argv) {
     dump_desc(f, S, cam);
   }
 
+  if (rt_abi_version() != RT_ABI_VERSION) {
+    std::cerr << "[ERROR] librtx_hip ABI version " << rt_abi_version() << ", this host was built for "
+              << RT_ABI_VERSION << "\n";
+    return 1;
+  }
   rt_frame frame;
   if (rt_camera_setup(&cam, &frame) != RT_OK) return fail_rt("camera");
   rt_scene_desc desc = S.desc();

@@ -5,6 +5,8 @@ sizes against the compiled library's own view (rt_abi_sizes) when available.
 """
 import ctypes as C
 
+RT_ABI_VERSION = 2  # include/rt_api.h; rtx/lib.py refuses a library of another version
+
 RT_OK = 0
 RT_ERR_INVALID = -1
 RT_ERR_DEVICE = -2
@@ -60,7 +62,9 @@ class SceneDesc(C.Structure):
                 ("n_objects", C.c_int32), ("objects", C.POINTER(ObjectDesc)),
                 ("children", C.POINTER(C.c_int32)), ("n_children", C.c_int32),
                 ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32),
-                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32)]
+                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
+                ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
+                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32)]
 
 
 RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
@@ -112,7 +116,9 @@ class SceneInfo(C.Structure):
                 ("bvh_depth", C.c_int32), ("node_bytes", C.c_int32),
                 ("sphere_bytes", C.c_int32), ("quad_bytes", C.c_int32),
                 ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32),
-                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32)]
+                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
+                ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
+                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

@@ -57,8 +57,9 @@ def load():
     L.rt_scene_bvh_cost.argtypes = [C.c_void_p, P(C.c_double)]
     for name in abi.EXPORTS:
         getattr(L, name).restype = C.c_char_p if name == "rt_last_error" else C.c_int
-    if L.rt_abi_version() != 1:
-        raise RuntimeError("rt ABI version mismatch")
+    if L.rt_abi_version() != abi.RT_ABI_VERSION:
+        raise RuntimeError("rt ABI version mismatch: library %d, bindings %d"
+                           % (L.rt_abi_version(), abi.RT_ABI_VERSION))
     _lib = L
     return L
 

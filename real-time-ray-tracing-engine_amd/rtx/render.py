@@ -99,6 +99,15 @@ class Renderer:
                                  out.ctypes.data_as(C.POINTER(C.c_double))))
         return out
 
+    def render_into(self, frame, host_ptr, seed=0, rows=(0, 0), samples=(0, -1),
+                    output=abi.RT_OUT_SCALED):
+        """rt_render into caller host memory at `host_ptr` (e.g. a pinned torch
+        tensor's data_ptr(), or a numpy buffer's address): kernel + D2H copy,
+        synchronous -- the reference's render_gpu batch loop."""
+        p = self.params(seed, rows, samples, output, 0)
+        check(self.lib.rt_render(self.handle, C.byref(frame), C.byref(p),
+                                 C.cast(C.c_void_p(host_ptr), C.POINTER(C.c_double))))
+
     def render_device(self, frame, dev_ptr, stream_ptr=None, seed=0, rows=(0, 0), samples=(0, -1),
                       output=abi.RT_OUT_SUM, accumulate=1, tiles=(0, 1), layout=abi.RT_LAYOUT_FRAME,
                       chunks=1):

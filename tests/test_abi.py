@@ -25,7 +25,10 @@ def header_functions():
 def test_library_built_and_loads():
     assert os.path.exists(LIB_PATH), "build/librtx_hip.so missing"
     L = load()
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == abi.RT_ABI_VERSION
+    # the bindings' version is the header's
+    m = re.search(r"^#define RT_ABI_VERSION (\d+)", open(HEADER).read(), re.M)
+    assert m and int(m.group(1)) == abi.RT_ABI_VERSION == 2
 
 
 def test_every_declared_symbol_is_exported():

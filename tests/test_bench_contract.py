@@ -35,8 +35,10 @@ def test_bench_line(layout):
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["dtype"] == "f64"
     assert d["value"] > 0 and d["unit"] == "Msamples/s"
     rf = d["roofline"]
-    assert rf["bound"] == "valu" and rf["kernel_ms"] > 0
-    assert 0 < rf["achieved"] <= 1 and rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-3)
+    assert rf["bound"] == "valu" and rf["unit"] == "TFLOP/s" and rf["kernel_ms"] > 0
+    assert rf["peak"] == 78.6 and 0 < rf["frac"] <= 1
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-3)
+    assert 0 < rf["valu_busy"] <= 1 and 0 < rf["f64_inst_share"] <= 1
     assert "committed" in rf["pmc_source"]
     assert d["config"]["width"] == 400 and d["config"]["spp"] == 9
     assert d["check"]["ok"], d["check"]
@@ -45,13 +47,14 @@ def test_bench_line(layout):
 @pytest.mark.gpu
 def test_bench_line_live_pmc():
     """Default --pmc auto: bench.py runs the rocprofv3 PMC passes (VALU, FETCH_SIZE,
-    WRITE_SIZE) on this build before its timed run; the roofline is the VALU-busy
-    fraction (<= 1) and traffic the PMC HBM bytes."""
+    WRITE_SIZE) on this build before its timed run; the roofline is the fp64
+    FLOP rate against the fp64 vector peak (<= 1), VALU-busy beside it, and
+    traffic the PMC HBM bytes."""
     d = _bench(timeout=400)
     rf = d["roofline"]
     assert rf["pmc_source"].startswith("live"), rf.get("pmc_source")
-    assert 0 < rf["frac"] <= 1 and rf["traffic"] > 0
-    assert rf["hbm"]["frac"] < 1
+    assert 0 < rf["frac"] <= 1 and rf["traffic"] > 0 and 0 < rf["valu_busy"] <= 1
+    assert rf["hbm_frac"] < 1
 
 
 def _free_port():
@@ -79,6 +82,11 @@ def test_bench_two_ranks_one_gpu(shard):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["check"]["ok"], d["check"]
+    # per-rank diagnostics: kernel ms of each rank, rank 0's exchange wait
+    rk = d["ranks"]
+    assert len(rk["per_rank_kernel_ms"]) == 2 and len(rk["per_rank_exchange_ms"]) == 2
+    assert 0 < rk["kernel_ms_min"] <= rk["kernel_ms_mean"] <= rk["kernel_ms_max"]
+    assert rk["exchange_ms_rank0"] >= 0 and rk["exchange_ms_max"] >= rk["exchange_ms_rank0"]
 
 
 @pytest.mark.gpu

@@ -88,3 +88,36 @@ def test_each_bvh4_instance_matches_oracle(F):
         assert info["features"] == F | abi.RT_FEAT_BVH4, info["features"]
         img = R.render(camera_frame(cam), seed=21)
     compare(img, O.oracle_render(S, cam, O.MODE_COUNTER, 21), 1e-4)
+
+
+def test_bvh4_kept_binary_when_its_stacks_do_not_fit_lds():
+    """A 4-wide walk pushes up to three entries per level, so its traversal
+    stacks take more LDS per block than the binary walk's one per level.  The
+    collapse is accepted only if the stacks (plus the static LDS) fit the
+    4-wide instance's per-block LDS share at its occupancy target; otherwise the
+    scene keeps the binary tree (LDS never lowers occupancy).  RTX_LDS_CAP lowers
+    the per-block share between the two trees' needs to force the fallback."""
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    cam = S.camera_desc(image_width=40, samples_per_pixel=4, max_depth=8)
+    f = camera_frame(cam)
+    i2, a, _ = render_arity(S, f, 2, 13)
+    i4, b, _ = render_arity(S, f, 4, 13)
+    assert i4["bvh_arity"] == 4 and i4["stack_depth"] > i2["stack_depth"]
+    for i in (i2, i4):
+        assert i["lds_fixed_bytes"] <= i["lds_block_budget"] <= 65536
+        assert i["lds_fixed_bytes"] + i["lds_nodes"] * i["node_bytes"] <= i["lds_block_budget"]
+    assert i4["lds_fixed_bytes"] > i2["lds_fixed_bytes"]
+    cap = (i2["lds_fixed_bytes"] + i4["lds_fixed_bytes"]) // 2
+    old = os.environ.get("RTX_LDS_CAP")
+    os.environ["RTX_LDS_CAP"] = str(cap)
+    try:
+        ic, c, _ = render_arity(S, f, 4, 13)
+    finally:
+        if old is None:
+            os.environ.pop("RTX_LDS_CAP")
+        else:
+            os.environ["RTX_LDS_CAP"] = old
+    assert ic["bvh_arity"] == 2 and not ic["features"] & abi.RT_FEAT_BVH4
+    assert ic["lds_fixed_bytes"] <= ic["lds_block_budget"] <= cap
+    assert np.array_equal(c, a)  # the same binary tree and walk
+    compare(b, a, 1e-12)

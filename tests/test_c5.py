@@ -1,0 +1,104 @@
+"""BASELINE config C5 at its own size: the 486-sphere "final scene" (motion
+blur, defocus, checker, glass; main.cpp:73-131 seeded to 42) at 3840x2160,
+spp 4096, depth 8 -- 129,600 8x8 tiles, 33.97 G samples per frame.
+
+* Two full-width 4K rows (crossing a tile-row boundary) against the oracle's
+  COUNTER mode at the full 4096 strata: the same per-channel 1e-4 bar as every
+  other parity test.
+* Whole-frame properties on the GPU, where the oracle cannot follow (a frame is
+  ~6 s on the GPU, days on the CPU):
+    - the stratum split [0, 2048) + [2048, 4096) adds up to the full frame and the
+      row split (top + bottom half) reassembles it (pixel and stratum indexing,
+      the Philox keys of a 4K frame, the per-launch chunk counts);
+    - the chunked frame launch (work units = (tile, stratum chunk), partials in
+      the scratch buffer, chunk_sum_kernel) equals the one-unit-per-tile launch
+      (no scratch) up to fp64 summation order -- the scratch / chunk sizing at
+      129,600 tiles;
+    - every channel finite, the image not black;
+    - the STATS instance's counters are exact where they can be (samples) and
+      consistent elsewhere, over the whole 4K frame.
+Reference: main.cpp:73-131 (scene), StaticCamera.cpp:235-300 (the batch loop
+this frame launch replaces).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from rtx import abi
+from rtx.render import Renderer, camera_frame
+from rtx.scene import load_scene
+import oracle_lib as O
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+SCENES = os.path.join(O.ROOT, "real-time-ray-tracing-engine_amd", "scenes")
+W, SPP, DEPTH = 3840, 4096, 8
+
+
+def c5_scene():
+    return load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+
+
+def test_c5_rows_match_oracle():
+    S = c5_scene()
+    cam = S.camera_desc(image_width=W, samples_per_pixel=SPP, max_depth=DEPTH)
+    f = camera_frame(cam)
+    assert (f.image_width, f.image_height, f.sqrt_spp) == (3840, 2160, 64)
+    rows = (1079, 1081)  # tile rows 134 / 135
+    with Renderer(S) as R:
+        gpu = R.render(f, seed=31, rows=rows)
+    ref = O.oracle_render(S, cam, O.MODE_COUNTER, 31, rows=rows, threads=16)
+    compare(gpu, ref)
+    assert np.nanmean(gpu) > 0
+
+
+def test_c5_full_frame_properties():
+    torch = pytest.importorskip("torch")
+    S = c5_scene()
+    cam = S.camera_desc(image_width=W, samples_per_pixel=SPP, max_depth=DEPTH)
+    f = camera_frame(cam)
+    H = f.image_height
+    dev = torch.device("cuda", 0)
+    full = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+    part = torch.empty_like(full)
+    with Renderer(S) as R:
+        info = R.info()
+        assert info["n_spheres"] == 486 and info["bvh_arity"] == 2
+        R.render_device(f, full.data_ptr(), 0, seed=17, output=abi.RT_OUT_SUM, accumulate=0)
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(full).all())
+        mean = float(full.mean()) / f.sqrt_spp ** 2
+        assert 0.05 < mean < 2.0, mean
+        # strata split: [0, 2048) then [2048, 4096) added on top
+        R.render_device(f, part.data_ptr(), 0, seed=17, samples=(0, 2048),
+                        output=abi.RT_OUT_SUM, accumulate=0)
+        R.render_device(f, part.data_ptr(), 0, seed=17, samples=(2048, 2048),
+                        output=abi.RT_OUT_SUM, accumulate=1)
+        torch.cuda.synchronize()
+        assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
+        # row split: the top and the bottom half into their own rows of `part`
+        half = H // 2
+        part.zero_()
+        R.render_device(f, part.data_ptr(), 0, seed=17, rows=(0, half), output=abi.RT_OUT_SUM,
+                        accumulate=0)
+        R.render_device(f, part[half:].data_ptr(), 0, seed=17, rows=(half, H),
+                        output=abi.RT_OUT_SUM, accumulate=0)
+        torch.cuda.synchronize()
+        assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
+        # one work unit per tile (no stratum chunks, no scratch buffer)
+        os.environ["RTX_CHUNK_TARGET"] = "0"
+        try:
+            R.render_device(f, part.data_ptr(), 0, seed=17, output=abi.RT_OUT_SUM, accumulate=0)
+            torch.cuda.synchronize()
+        finally:
+            del os.environ["RTX_CHUNK_TARGET"]
+        assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
+        # counters over the whole 4K frame (spp 16 keeps the STATS instance short)
+        cam16 = S.camera_desc(image_width=W, samples_per_pixel=16, max_depth=DEPTH)
+        st = R.stats(camera_frame(cam16), seed=17)
+    assert st["samples"] == W * H * 16
+    assert st["samples"] <= st["segments"] <= DEPTH * st["samples"]
+    assert 0 < st["shade_events"] <= st["segments"]
+    assert st["node_visits"] > st["segments"] and st["sphere_tests"] > 0
+    assert st["wave_trips"] > 0 and st["segments"] <= 64 * st["wave_trips"]

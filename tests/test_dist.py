@@ -181,3 +181,50 @@ def test_gpu_tile_layout_reassembles_bit_exact():
         one = R.render(f, seed=6, output=abi.RT_OUT_SUM, tiles=(1, world),
                        layout=abi.RT_LAYOUT_TILES)
     np.testing.assert_allclose(ch.sum(axis=1), one, rtol=1e-12, atol=1e-13)
+
+
+# ------------------------------------------------------ bench.py N>1 diagnostics
+def _diag_worker(rank, world, port, out_path):
+    import json
+    import sys
+    sys.path.insert(0, O.ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        S = load_scene(SCENE)
+        cam = S.camera_desc(image_width=16, samples_per_pixel=4, max_depth=4)
+        acc = torch.zeros((9, 16, 3), dtype=torch.float64)
+
+        def launch_work(seed, b):  # rank 1 renders twice as much: a visible imbalance
+            for _ in range(1 + rank):
+                acc.copy_(torch.from_numpy(O.oracle_render(S, cam, O.MODE_COUNTER, seed,
+                                                           output=abi.RT_OUT_SUM)))
+
+        def exchange(b):
+            return dist.all_reduce(acc, op=dist.ReduceOp.SUM, async_op=True)
+
+        d = bench.rank_diagnostics(torch, dist, torch.device("cpu"), rank, world, launch_work,
+                                   exchange, lambda w: w.wait() if w is not None else None)
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(d, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_diagnostics_two_gloo_ranks(tmp_path):
+    """bench.py's N>1 diagnostics (the fields an 8-GPU line carries): each rank's
+    render time, min / mean / max over ranks, and rank 0's exchange wait, which
+    includes waiting for the slower rank."""
+    import json
+    out = str(tmp_path / "diag.json")
+    mp.spawn(_diag_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    d = json.load(open(out))
+    k = d["per_rank_kernel_ms"]
+    assert len(k) == 2 and len(d["per_rank_exchange_ms"]) == 2
+    assert d["kernel_ms_min"] == min(k) and d["kernel_ms_max"] == max(k)
+    assert k[1] > k[0]  # rank 1 did twice the work
+    # rank 0 finished first, so its exchange waits for rank 1's extra render
+    assert d["exchange_ms_rank0"] > 0.3 * (k[1] - k[0])

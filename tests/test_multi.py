@@ -36,6 +36,10 @@ def test_multi_create_validates_before_device_use():
     assert L.rt_multi_create(C.byref(d), devs, 2, 1, C.byref(h)) == abi.RT_ERR_INVALID
     assert b"n_shards" in L.rt_last_error()
     assert L.rt_multi_create(C.byref(d), devs, 0, 1, C.byref(h)) == abi.RT_ERR_INVALID
+    # shard count bounded (a device scene copy + a host thread each): refused
+    # before any scene is created
+    assert L.rt_multi_create(C.byref(d), devs, 1, 257, C.byref(h)) == abi.RT_ERR_INVALID
+    assert b"RT_MULTI_MAX_SHARDS" in L.rt_last_error()
     assert L.rt_multi_render(None, None, None, None) == abi.RT_ERR_INVALID
     assert L.rt_multi_destroy(None) == abi.RT_OK
 
