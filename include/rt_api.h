@@ -298,6 +298,9 @@ typedef struct rt_scene_info {
   int32_t lds_block_budget; /* LDS per block at the kernel's occupancy target; the node prefix
                                fills what lds_fixed_bytes leaves (LDS never lowers occupancy) */
   int32_t waves_per_simd;   /* occupancy target of the kernel instance the scene selects */
+  int32_t lds_nodes_persistent; /* BVH nodes staged by the persistent frame instance (one
+                                   16-wave block per CU owning its 160 KB of LDS); -1: the
+                                   scene's frames run one work unit per wavefront */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

@@ -26,6 +26,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
 extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *n_nodes);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
 extern "C" size_t rtk_sah_temp_bytes(int n);
 extern "C" hipError_t rtk_build_sah(const double *boxes, const DItem *items_in, int n,
@@ -453,6 +454,14 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     int budget = plan.n_nodes;
     if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
+    int pc_nodes = -1; // the persistent instance's prefix (-1: no persistent launches)
+    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pc_nodes);
+    if (be != hipSuccess) {
+      rt_scene_destroy(s);
+      return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
+    }
+    if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) pc_nodes = std::atoi(ln); // A/B experiments
+    d.n_lds_nodes_pc = pc_nodes < 0 ? -1 : std::min(pc_nodes, d.n_nodes);
   }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
   s->unit_ctr = (int32_t *)(s->block + parts[iUc].off);
@@ -478,6 +487,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.lds_fixed_bytes = plan.fixed_bytes;
   in.lds_block_budget = plan.block_budget;
   in.waves_per_simd = plan.waves_per_simd;
+  in.lds_nodes_persistent = d.n_lds_nodes_pc;
   *out = s;
   return RT_OK;
 }
@@ -547,7 +557,7 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   DLaunch Lp = L;
   if (persistent && s->wave_slots > 0) {
     Lp.unit_ctr = s->unit_ctr;
-    Lp.grid_cap = std::max(1, s->wave_slots / 4);
+    Lp.grid_cap = std::max(1, s->wave_slots / RT_PC_BLOCK_WAVES); // one persistent block per CU
     // RT_GRID_CAP: fewer resident blocks (tests: many units per wave)
     if (const char *g = getenv("RT_GRID_CAP"))
       if (atoi(g) > 0) Lp.grid_cap = atoi(g);

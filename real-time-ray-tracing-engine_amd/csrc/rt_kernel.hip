@@ -52,6 +52,15 @@ using namespace rtp;
 #define RT_BLOCK_WAVES 4
 #endif
 constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
+// Waves per block of the persistent instance: one block per CU (16 = 4 SIMDs x
+// its 4-waves/SIMD target), so the CU's 160 KB of LDS holds ONE copy of the
+// staged BVH beside its 16 waves' stacks instead of four copies for four
+// 4-wave blocks (gfx950: a workgroup may own all 160 KB).
+#ifndef RT_PC_WAVES
+#define RT_PC_WAVES 16
+#endif
+constexpr int kPcWaves = RT_PC_WAVES;
+constexpr size_t kLdsPerCu = 160 * 1024;
 
 // Occupancy target per instance (waves per SIMD): the compiler may spill a few
 // registers to reach it.  Measured: 4 for the plain instance (C3
@@ -145,6 +154,85 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
     return P;
   }
 }
+// The camera read afresh from the kernarg segment where it is used (FRESH: the
+// rich instances, whose scene tables and path state leave no SGPRs for the
+// camera's 52 dwords across the path loop -- held there, they spilled into
+// VGPR lanes and every use cost a v_readlane).  Scalar loads through the
+// asm-hidden segment pointer: they stay at the use, the scalar cache serves them.
+#ifndef RT_CAM_FRESH
+#define RT_CAM_FRESH 1
+#endif
+#ifndef RT_CAM_FRESH_F
+#define RT_CAM_FRESH_F(F) (RT_CAM_FRESH != 0 && ((F) & (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE)) != 0)
+#endif
+template <bool FRESH>
+__device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
+  if constexpr (FRESH) {
+    auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const __attribute__((address_space(4))) DCamera &K = ka->C;
+    DCamera D;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      D.center[k] = K.center[k];
+      D.p00[k] = K.p00[k];
+      D.du[k] = K.du[k];
+      D.dv[k] = K.dv[k];
+      D.disk_u[k] = K.disk_u[k];
+      D.disk_v[k] = K.disk_v[k];
+      D.bg[k] = K.bg[k];
+    }
+    D.defocus_angle = K.defocus_angle;
+    D.scale = K.scale;
+    D.rs = K.rs;
+    D.W = K.W;
+    D.H = K.H;
+    D.sqrt_spp = K.sqrt_spp;
+    D.max_depth = K.max_depth;
+    return D;
+  } else {
+    return C;
+  }
+}
+// The scene tables read afresh at each path segment (FRESH: A/B experiments).
+#ifndef RT_SCENE_FRESH
+#define RT_SCENE_FRESH 0
+#endif
+template <bool FRESH>
+__device__ __forceinline__ DScene scene_fields(const DScene &S) {
+  if constexpr (FRESH) {
+    auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const __attribute__((address_space(4))) DScene &K = ka->S;
+    DScene D;
+    D.nodes = K.nodes;
+    D.items = K.items;
+    D.mitems = K.mitems;
+    D.mbox = K.mbox;
+    D.bitems = K.bitems;
+    D.xforms = K.xforms;
+    D.spheres = K.spheres;
+    D.quads = K.quads;
+    D.media = K.media;
+    D.mats = K.mats;
+    D.texs = K.texs;
+    D.perlin = K.perlin;
+    D.lights = K.lights;
+    D.n_lights = K.n_lights;
+    D.n_nodes = K.n_nodes;
+    D.root_is_leaf = K.root_is_leaf;
+    D.n_root_items = K.n_root_items;
+    D.features = K.features;
+    D.n_mitems = K.n_mitems;
+    D.stack_depth = K.stack_depth;
+    D.n_lds_nodes = S.n_lds_nodes; // the instance's own prefix (PC: n_lds_nodes_pc)
+    D.static_spheres = K.static_spheres;
+    D.n_lds_nodes_pc = K.n_lds_nodes_pc;
+    return D;
+  } else {
+    return S;
+  }
+}
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -161,19 +249,24 @@ __device__ __forceinline__ double *out_arg(double *out) {
 // sums), whose waves persist and pull units; the launch fields those launches
 // fix are constants here, so they are not live across the path loop.
 template <bool STATS, unsigned F, bool PC = false>
-__global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
-  // dynamic LDS: traversal stacks [kWaves][S.stack_depth][64] ints, then the
+  constexpr int BW = PC ? kPcWaves : kWaves; // waves per block
+  constexpr bool kCamFresh = RT_CAM_FRESH_F(F);
+  // the persistent instance stages its own (larger) node prefix
+  DScene S = S_;
+  if constexpr (PC) S.n_lds_nodes = S_.n_lds_nodes_pc;
+  // dynamic LDS: traversal stacks [BW][S.stack_depth][64] ints, then the
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
   extern __shared__ int4 dyn_lds[];
-  __shared__ double acc_lds[kWaves][64][3];
+  __shared__ double acc_lds[BW][64][3];
   // compacted leaf tests (BVH instances only; 1 KB per wave)
-  __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? kWaves : 1];
+  __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? BW : 1];
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   int *stack_base = reinterpret_cast<int *>(dyn_lds);
-  DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + kWaves * S.stack_depth * 64);
+  DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + BW * S.stack_depth * 64);
   const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g; // DNode4 in BVH4 instances
   constexpr int kNodeBytes = (F & F_BVH4) ? (int)sizeof(DNode4) : (int)sizeof(DNode);
   if (S.n_lds_nodes > 0) { // stage the top of the BVH (BFS prefix) once per block
@@ -189,7 +282,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
   // the grid's wave count), so waves take new units as they finish instead of
   // waiting for their block.
   const int n_units = P.n_local_tiles * P.n_chunks;
-  int unit = blockIdx.x * kWaves + wv;
+  int unit = blockIdx.x * BW + wv;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
   double *acc = &acc_lds[wv][0][0];
   Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -232,17 +325,18 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
       int item = next_item + rank;
       next_item += __popcll(idle);
       if (!ps.active && item < n_items) {
+        const DCamera Cr = camera_fields<kCamFresh>(C);
         int slot = item & 63;
         int i = x0 + (slot & 7), j = y0 + (slot >> 3);
-        if (i < C.W && j < P.row_end) {
+        if (i < Cr.W && j < P.row_end) {
           ps.slot = slot;
           ps.sample = s_first + (item >> 6);
-          key.pixel = (uint32_t)(j * C.W + i);
+          key.pixel = (uint32_t)(j * Cr.W + i);
           key.sample = (uint32_t)ps.sample;
-          ps.ray = camera_ray<F == F_FLAT>(C, key, i, j, ps.sample);
+          ps.ray = camera_ray<F == F_FLAT>(Cr, key, i, j, ps.sample);
           ps.T = v3(1.0, 1.0, 1.0);
           ps.bounce = 0;
-          ps.active = C.max_depth > 0;
+          ps.active = Cr.max_depth > 0;
           if (STATS) n_samples++;
         }
       }
@@ -252,7 +346,7 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS, F>(S, C, ps, key, stk, lnodes, cnt,
+      bool cont = segment<STATS, F>(scene_fields<RT_SCENE_FRESH && kCamFresh>(S), camera_fields<kCamFresh>(C), ps, key, stk, lnodes, cnt,
                                     (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0]);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
@@ -266,18 +360,19 @@ __global__ __launch_bounds__(64 * RT_BLOCK_WAVES) __attribute__((amdgpu_waves_pe
 
   // ---- tile epilogue: one coalesced store per pixel
   {
+    const DCamera Ce = camera_fields<kCamFresh>(C);
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
     const bool compact = PC || P.compact;
-    if (compact || (i < C.W && j < P.row_end)) { // tile slots outside the image hold 0
+    if (compact || (i < Ce.W && j < P.row_end)) { // tile slots outside the image hold 0
       double sx = acc[lane * 3 + 0], sy = acc[lane * 3 + 1], sz = acc[lane * 3 + 2];
       if (!PC && P.output == RT_OUT_SCALED) {
-        sx = C.scale * sx;
-        sy = C.scale * sy;
-        sz = C.scale * sz;
+        sx = Ce.scale * sx;
+        sy = Ce.scale * sy;
+        sz = Ce.scale * sz;
       }
       double *const ob = out_arg<PC && RT_KARG_FRESH>(out);
       double *o = compact ? ob + 3 * ((size_t)unit * 64 + lane)
-                            : out + 3 * ((size_t)(j - P.row_begin) * C.W + i);
+                            : out + 3 * ((size_t)(j - P.row_begin) * Ce.W + i);
       if (!PC && P.accumulate) {
         o[0] += sx;
         o[1] += sy;
@@ -374,6 +469,11 @@ extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) 
   const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
   return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
+// the persistent instance's dynamic LDS (kPcWaves waves per block)
+static size_t lds_bytes_pc(int features, int stack_depth, int n_lds_nodes) {
+  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  return (size_t)kPcWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
+}
 
 // LDS plan per block at the occupancy the instance's register count allows
 // (blocks of kWaves waves over the 4 SIMDs): the bytes left for the staged BVH
@@ -404,28 +504,54 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   return hipSuccess;
 }
 
+// Node prefix of the persistent instance (one kPcWaves-wave block per CU,
+// which may own the CU's whole LDS): -1 when its stacks alone do not fit, or
+// the feature set has no persistent instance.
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *n_nodes) {
+  *n_nodes = -1;
+  const unsigned f = (unsigned)(features & F_ALL);
+  if (!RT_PERSIST_F(f)) return hipSuccess;
+  RenderFn fn = persistent_instance(f);
+  hipFuncAttributes a;
+  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fn));
+  if (e != hipSuccess) return e;
+  const size_t fixed = a.sharedSizeBytes + lds_bytes_pc(features, stack_depth, 0);
+  if (fixed > kLdsPerCu) return hipSuccess;
+  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  *n_nodes = (int)((kLdsPerCu - fixed) / node);
+  return hipSuccess;
+}
+
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
-  int blocks = (P->n_local_tiles * P->n_chunks + kWaves - 1) / kWaves;
+  const int64_t units = (int64_t)P->n_local_tiles * P->n_chunks;
+  int blocks = (int)((units + kWaves - 1) / kWaves);
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
+  int block_waves = kWaves;
   DLaunch Q = *P;
   const unsigned f = (unsigned)(S->features & F_ALL);
   if (RT_PERSIST_F(f) && stats == nullptr && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
-      blocks > Q.grid_cap && Q.compact && Q.output == RT_OUT_SUM && !Q.accumulate &&
-      Q.tile_first == 0 && Q.tile_stride == 1) {
-    // persistent: the resident blocks' waves take units [0, grid_cap * kWaves)
+      S->n_lds_nodes_pc >= 0 && units > (int64_t)Q.grid_cap * kPcWaves && Q.compact &&
+      Q.output == RT_OUT_SUM && !Q.accumulate && Q.tile_first == 0 && Q.tile_stride == 1) {
+    // persistent: the resident blocks' waves take units [0, grid_cap * kPcWaves)
     // statically, the rest from the counter
     fn = persistent_instance(f);
     blocks = Q.grid_cap;
-    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * kWaves, 1, stream);
+    block_waves = kPcWaves;
+    lds = lds_bytes_pc(S->features, S->stack_depth, S->n_lds_nodes_pc);
+    // beyond 64 KB of LDS per block (set on every launch: cheap, and per device)
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * kPcWaves, 1, stream);
     if (e != hipSuccess) return e;
   } else {
     Q.unit_ctr = nullptr; // every unit has its own wave
   }
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWaves), lds, stream, *S, *C, Q, out, stats);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * block_waves), lds, stream, *S, *C, Q, out, stats);
   return hipGetLastError();
 }
 

@@ -29,6 +29,10 @@
 #define RT_N_STATS 18      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 #define RT_STACK_DEPTH4 64 // 4-wide walks push up to three entries per level
+#ifndef RT_PC_WAVES
+#define RT_PC_WAVES 16    // waves per block of the persistent instance (one block per CU)
+#endif
+#define RT_PC_BLOCK_WAVES RT_PC_WAVES
 #ifndef RT_FLAT_MAX
 #define RT_FLAT_MAX 8 // worlds of at most this many items are one flat leaf (no BVH walk)
 #endif
@@ -164,6 +168,8 @@ struct DScene {      // kernel argument (by value)
   int32_t stack_depth;   // per-lane traversal stack entries (BVH depth + 1)
   int32_t n_lds_nodes;   // nodes [0, n_lds_nodes) are staged in LDS (BFS order: top levels)
   int32_t static_spheres; // 1: every sphere has c1 == c0 (no motion blur): center = c0
+  int32_t n_lds_nodes_pc; // nodes staged by the persistent instance's one-per-CU blocks
+                          // (-1: its stacks do not fit, no persistent launches)
 };
 
 // Scene features (kernel specialisation keys)

@@ -64,7 +64,8 @@ class SceneDesc(C.Structure):
                 ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32),
                 ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
-                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32)]
+                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
+                ("lds_nodes_persistent", C.c_int32)]
 
 
 RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
@@ -118,7 +119,8 @@ class SceneInfo(C.Structure):
                 ("device_bytes", C.c_int64), ("features", C.c_int32), ("lds_nodes", C.c_int32),
                 ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
-                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32)]
+                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
+                ("lds_nodes_persistent", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).
