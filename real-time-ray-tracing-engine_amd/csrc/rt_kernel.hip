@@ -162,6 +162,9 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
 #ifndef RT_CAM_FRESH
 #define RT_CAM_FRESH 1
 #endif
+#ifndef RT_CAM_FRESH_SEG
+#define RT_CAM_FRESH_SEG 0 // also at every path segment (background, depth budget)
+#endif
 #ifndef RT_CAM_FRESH_F
 #define RT_CAM_FRESH_F(F) (RT_CAM_FRESH != 0 && ((F) & (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE)) != 0)
 #endif
@@ -346,7 +349,8 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS, F>(scene_fields<RT_SCENE_FRESH && kCamFresh>(S), camera_fields<kCamFresh>(C), ps, key, stk, lnodes, cnt,
+      bool cont = segment<STATS, F>(scene_fields<RT_SCENE_FRESH && kCamFresh>(S),
+                                    camera_fields<RT_CAM_FRESH_SEG && kCamFresh>(C), ps, key, stk, lnodes, cnt,
                                     (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0]);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);

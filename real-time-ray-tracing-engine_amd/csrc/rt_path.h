@@ -774,6 +774,37 @@ RT_HD RT_FI float slab(const RayF<FMA> &q, const float *lo, const float *hi, flo
   else
     return tl <= th * kSlabGrow ? tl : __builtin_huge_valf();
 }
+// The same test as slab<FMA=true> with the verdict and the entry distance
+// returned apart: the binary node visit branches on the verdict and orders the
+// two children by the entry distances, so selecting +inf for a miss and
+// comparing against it again (two VALU per box) is not needed.
+RT_HD RT_FI bool slab_hit(const RayF<true> &q, const float *lo, const float *hi, float tmin32,
+                          float cl32, float &tl) {
+  const float a0 = fmaf(lo[0], q.inv[0], -q.p[0]), b0 = fmaf(hi[0], q.inv[0], -q.p[0]);
+  const float a1 = fmaf(lo[1], q.inv[1], -q.p[1]), b1 = fmaf(hi[1], q.inv[1], -q.p[1]);
+  const float a2 = fmaf(lo[2], q.inv[2], -q.p[2]), b2 = fmaf(hi[2], q.inv[2], -q.p[2]);
+  tl = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), tmin32));
+#if defined(__HIP_DEVICE_COMPILE__)
+  // min(x, cl32) as v_min3_f32 in asm: cl32 is a loop-carried value the
+  // compiler cannot prove canonical, so fminf re-canonicalised it (one v_max)
+  // at every node visit; both operands are the results of float operations
+  float th;
+  const float m01 = fminf(fmaxf(a0, b0), fmaxf(a1, b1));
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(th) : "v"(fmaxf(a2, b2)), "v"(cl32), "v"(m01));
+#else
+  const float th = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), cl32));
+#endif
+  return tl <= fmaf(th, kSlabGrow, q.slack);
+}
+// f32_up(x) as a canonical float (the min/max operations take it as is
+// instead of re-canonicalising it at every box test)
+RT_HD RT_FI float f32_up_c(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_canonicalizef(f32_up(x));
+#else
+  return f32_up(x);
+#endif
+}
 
 // Per-wave LDS scratch of the compacted leaf tests (trace, leaf_share): the
 // round's (item << 6 | owner lane) table and each owner's running closest t
@@ -946,7 +977,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     const bool hit = item_root(ii, r, a, ya, closest, t);
     if (hit) {
       closest = t;
-      if constexpr (kBoxes) cl32 = f32_up(closest);
+      if constexpr (kBoxes) cl32 = f32_up_c(closest);
       best = ii;
     }
   };
@@ -1028,7 +1059,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         ckey = nk;
         closest = __longlong_as_double((long long)nb);
         best = pool->bi[lane];
-        if constexpr (kBoxes) cl32 = f32_up(closest);
+        if constexpr (kBoxes) cl32 = f32_up_c(closest);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -1138,10 +1169,16 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         } else {
           N = S.nodes[cur];
         }
+#if RT_SLAB_FMA
+        float tn0, tn1;
+        const bool h0 = slab_hit(q, N.lo0, N.hi0, tmin32, cl32, tn0);
+        const bool h1 = slab_hit(q, N.lo1, N.hi1, tmin32, cl32, tn1);
+#else
         const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
         const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
-        const int e0 = N.entry[0], e1 = N.entry[1];
         const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
+#endif
+        const int e0 = N.entry[0], e1 = N.entry[1];
         if (h0 && h1) {
           const bool first0 = tn0 <= tn1;
           if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
