@@ -301,6 +301,8 @@ typedef struct rt_scene_info {
   int32_t lds_nodes_persistent; /* BVH nodes staged by the persistent frame instance (one
                                    16-wave block per CU owning its 160 KB of LDS); -1: the
                                    scene's frames run one work unit per wavefront */
+  int32_t lds_prims_persistent; /* 1: the persistent frame instance also stages every world
+                                   item and sphere in LDS (whole tree staged and room left) */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

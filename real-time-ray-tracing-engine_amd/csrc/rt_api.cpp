@@ -26,7 +26,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
 extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *n_nodes);
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int64_t *free_bytes);
+extern "C" int rtk_lds_prims_enabled(void);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
 extern "C" size_t rtk_sah_temp_bytes(int n);
 extern "C" hipError_t rtk_build_sah(const double *boxes, const DItem *items_in, int n,
@@ -454,14 +455,28 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     int budget = plan.n_nodes;
     if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
-    int pc_nodes = -1; // the persistent instance's prefix (-1: no persistent launches)
-    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pc_nodes);
+    // the persistent instance: its node prefix, then -- if the whole tree is
+    // staged and room is left -- the world items and spheres (-1: no
+    // persistent launches)
+    int64_t pc_free = -1;
+    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pc_free);
     if (be != hipSuccess) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
     }
-    if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) pc_nodes = std::atoi(ln); // A/B experiments
-    d.n_lds_nodes_pc = pc_nodes < 0 ? -1 : std::min(pc_nodes, d.n_nodes);
+    const int64_t node_b = (d.features & RT_FEAT_BVH4) ? (int64_t)sizeof(DNode4) : (int64_t)sizeof(DNode);
+    d.n_lds_nodes_pc = pc_free < 0 ? -1 : (int32_t)std::min<int64_t>(pc_free / node_b, d.n_nodes);
+    if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) // A/B experiments
+      if (d.n_lds_nodes_pc >= 0) d.n_lds_nodes_pc = std::min(std::atoi(ln), d.n_nodes);
+    d.lds_items_pc = d.lds_spheres_pc = 0;
+    const int64_t prim_b = (int64_t)(H.items.size() * sizeof(DItem) + H.spheres.size() * sizeof(DSphere));
+    const char *lp_env = std::getenv("RTX_LDS_PRIMS"); // 0: A/B experiments
+    if (rtk_lds_prims_enabled() && !(lp_env && lp_env[0] == '0') && pc_free >= 0 &&
+        d.n_lds_nodes_pc == d.n_nodes && pc_free - (int64_t)d.n_nodes * node_b >= prim_b &&
+        !H.items.empty()) {
+      d.lds_items_pc = (int32_t)H.items.size();
+      d.lds_spheres_pc = (int32_t)H.spheres.size();
+    }
   }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
   s->unit_ctr = (int32_t *)(s->block + parts[iUc].off);
@@ -488,6 +503,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.lds_block_budget = plan.block_budget;
   in.waves_per_simd = plan.waves_per_simd;
   in.lds_nodes_persistent = d.n_lds_nodes_pc;
+  in.lds_prims_persistent = d.lds_items_pc > 0;
   *out = s;
   return RT_OK;
 }

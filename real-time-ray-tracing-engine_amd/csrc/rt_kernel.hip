@@ -60,6 +60,10 @@ constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
 #define RT_PC_WAVES 16
 #endif
 constexpr int kPcWaves = RT_PC_WAVES;
+// the persistent instance also stages the world items and spheres when they fit
+#ifndef RT_LDS_PRIMS
+#define RT_LDS_PRIMS 1
+#endif
 constexpr size_t kLdsPerCu = 160 * 1024;
 
 // Occupancy target per instance (waves per SIMD): the compiler may spill a few
@@ -114,12 +118,12 @@ struct KArgs {
 // here instead of silently shifting what the persistent instance reads (its
 // frames are also checked bit for bit against the one-unit-per-wave instance
 // on the GPU: tests/test_persistent.py, and through every BASELINE band).
-static_assert(sizeof(DScene) == 144 && alignof(DScene) == 8, "DScene kernarg layout");
+static_assert(sizeof(DScene) == 152 && alignof(DScene) == 8, "DScene kernarg layout");
 static_assert(sizeof(DCamera) == 208 && alignof(DCamera) == 8, "DCamera kernarg layout");
 static_assert(sizeof(DLaunch) == 80 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
-static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 144 && offsetof(KArgs, P) == 352 &&
-                  offsetof(KArgs, out) == 432 && offsetof(KArgs, stats) == 440 &&
-                  sizeof(KArgs) == 448,
+static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 152 && offsetof(KArgs, P) == 360 &&
+                  offsetof(KArgs, out) == 440 && offsetof(KArgs, stats) == 448 &&
+                  sizeof(KArgs) == 456,
               "KArgs must mirror render_tiles' kernarg layout");
 static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
                   offsetof(DLaunch, grid_cap) == 72,
@@ -160,7 +164,7 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
 // VGPR lanes and every use cost a v_readlane).  Scalar loads through the
 // asm-hidden segment pointer: they stay at the use, the scalar cache serves them.
 #ifndef RT_CAM_FRESH
-#define RT_CAM_FRESH 1
+#define RT_CAM_FRESH 0 // measured: C4 -17 % (every segment), -21 % (regeneration only); profiles/r03b_ab.log, r03c_ab.log
 #endif
 #ifndef RT_CAM_FRESH_SEG
 #define RT_CAM_FRESH_SEG 0 // also at every path segment (background, depth budget)
@@ -231,6 +235,8 @@ __device__ __forceinline__ DScene scene_fields(const DScene &S) {
     D.n_lds_nodes = S.n_lds_nodes; // the instance's own prefix (PC: n_lds_nodes_pc)
     D.static_spheres = K.static_spheres;
     D.n_lds_nodes_pc = K.n_lds_nodes_pc;
+    D.lds_items_pc = K.lds_items_pc;
+    D.lds_spheres_pc = K.lds_spheres_pc;
     return D;
   } else {
     return S;
@@ -272,11 +278,29 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
   DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + BW * S.stack_depth * 64);
   const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g; // DNode4 in BVH4 instances
   constexpr int kNodeBytes = (F & F_BVH4) ? (int)sizeof(DNode4) : (int)sizeof(DNode);
-  if (S.n_lds_nodes > 0) { // stage the top of the BVH (BFS prefix) once per block
+  // persistent instance: world items and spheres after the nodes (LdsPrims)
+  LdsPrims lp{nullptr, nullptr};
+  int4 *prim_g = reinterpret_cast<int4 *>(lnodes_g) + (size_t)max(0, S.n_lds_nodes) * (kNodeBytes / 16);
+  if constexpr (PC) {
+    if (S.lds_items_pc > 0) {
+      lp.items = (const RT_LDS DItem *)reinterpret_cast<DItem *>(prim_g);
+      lp.spheres = (const RT_LDS DSphere *)reinterpret_cast<DSphere *>(prim_g + (size_t)S.lds_items_pc * 2);
+    }
+  }
+  if (S.n_lds_nodes > 0 || (PC && S.lds_items_pc > 0)) { // stage once per block
     const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
     int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
-    const int n16 = S.n_lds_nodes * (kNodeBytes / 16);
+    const int n16 = max(0, S.n_lds_nodes) * (kNodeBytes / 16);
     for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    if constexpr (PC) {
+      if (S.lds_items_pc > 0) {
+        const int ni = S.lds_items_pc * 2, ns = S.lds_spheres_pc * 4; // int4 per DItem / DSphere
+        const int4 *si = reinterpret_cast<const int4 *>(S.items);
+        const int4 *ss = reinterpret_cast<const int4 *>(S.spheres);
+        for (int k = threadIdx.x; k < ni; k += blockDim.x) prim_g[k] = si[k];
+        for (int k = threadIdx.x; k < ns; k += blockDim.x) prim_g[ni + k] = ss[k];
+      }
+    }
     __syncthreads();
   }
   // work unit = (local tile, stratum chunk).  Persistent launches (P.unit_ctr
@@ -349,9 +373,9 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     if (ps.active) {
       if (STATS) n_segments++;
-      bool cont = segment<STATS, F>(scene_fields<RT_SCENE_FRESH && kCamFresh>(S),
-                                    camera_fields<RT_CAM_FRESH_SEG && kCamFresh>(C), ps, key, stk, lnodes, cnt,
-                                    (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0]);
+      bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
+          scene_fields<RT_SCENE_FRESH && kCamFresh>(S), camera_fields<RT_CAM_FRESH_SEG && kCamFresh>(C), ps,
+          key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
@@ -508,11 +532,12 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   return hipSuccess;
 }
 
-// Node prefix of the persistent instance (one kPcWaves-wave block per CU,
-// which may own the CU's whole LDS): -1 when its stacks alone do not fit, or
-// the feature set has no persistent instance.
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *n_nodes) {
-  *n_nodes = -1;
+// LDS the persistent instance (one kPcWaves-wave block per CU, which may own
+// the CU's whole LDS) has left for staging after its stacks and static LDS:
+// -1 when the stacks alone do not fit, or the feature set has no persistent
+// instance.
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int64_t *free_bytes) {
+  *free_bytes = -1;
   const unsigned f = (unsigned)(features & F_ALL);
   if (!RT_PERSIST_F(f)) return hipSuccess;
   RenderFn fn = persistent_instance(f);
@@ -521,10 +546,10 @@ extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *n_node
   if (e != hipSuccess) return e;
   const size_t fixed = a.sharedSizeBytes + lds_bytes_pc(features, stack_depth, 0);
   if (fixed > kLdsPerCu) return hipSuccess;
-  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
-  *n_nodes = (int)((kLdsPerCu - fixed) / node);
+  *free_bytes = (int64_t)(kLdsPerCu - fixed);
   return hipSuccess;
 }
+extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
 
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
@@ -545,7 +570,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
     fn = persistent_instance(f);
     blocks = Q.grid_cap;
     block_waves = kPcWaves;
-    lds = lds_bytes_pc(S->features, S->stack_depth, S->n_lds_nodes_pc);
+    lds = lds_bytes_pc(S->features, S->stack_depth, S->n_lds_nodes_pc) +
+          (size_t)S->lds_items_pc * sizeof(DItem) + (size_t)S->lds_spheres_pc * sizeof(DSphere);
     // beyond 64 KB of LDS per block (set on every launch: cheap, and per device)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -170,6 +170,8 @@ struct DScene {      // kernel argument (by value)
   int32_t static_spheres; // 1: every sphere has c1 == c0 (no motion blur): center = c0
   int32_t n_lds_nodes_pc; // nodes staged by the persistent instance's one-per-CU blocks
                           // (-1: its stacks do not fit, no persistent launches)
+  int32_t lds_items_pc;   // world items [0, n) and spheres [0, lds_spheres_pc) the persistent
+  int32_t lds_spheres_pc; // instance stages after its nodes (0: primitives stay in HBM)
 };
 
 // Scene features (kernel specialisation keys)

@@ -124,6 +124,29 @@ struct Hit {
   bool front;
 };
 
+// ------------------------------------------------------- uniform loads
+// A scene-table record whose index is the same in every lane of the wavefront
+// (the flat list walk, the media and light-pdf loops): read through the
+// constant address space, so the compiler issues one scalar load (s_load)
+// into SGPRs instead of a vector load per lane into VGPRs -- no VMEM
+// instruction, no per-lane address arithmetic, no VGPRs for the record.  The
+// scene tables are never written while a kernel runs.  U = false: a plain load.
+template <bool U>
+struct UTag {
+  static constexpr bool value = U;
+};
+template <bool U, class T>
+RT_HD RT_FI T ldu(const T *p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (U) {
+    T t;
+    __builtin_memcpy(&t, (const __attribute__((address_space(4))) T *)(p + i), sizeof(T));
+    return t;
+  }
+#endif
+  return p[i];
+}
+
 // ---------------------------------------------------------------- RNG
 struct Key {
   uint32_t k0, k1, pixel, sample;
@@ -419,27 +442,38 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
 #ifndef RT_QUAD_AA
 #define RT_QUAD_AA 1
 #endif
+#ifndef RT_UNIFORM_LOADS
+#define RT_UNIFORM_LOADS 1 // scalar loads of wave-uniform scene records (ldu)
+#endif
 RT_HD RT_FI double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); } // no private array
+// SEL: the quad's axis components picked by value selects, not by an indexed
+// load -- for a record held in registers (a uniform scalar load, ldu), where
+// an indexed access would put it in scratch memory
+template <bool SEL = false>
 RT_HD RT_FI bool quad_t_aa(const DQuad &q, const Ray &r, double tmin, double tmax, double &t) {
   const int k = q.aa & 3, i = (q.aa >> 2) & 3, j = (q.aa >> 4) & 3;
-  const double denom = q.n[k] * comp(r.d, k);
+  const double nk = SEL ? comp(ld3(q.n), k) : q.n[k], wk = SEL ? comp(ld3(q.w), k) : q.w[k];
+  const double Qi = SEL ? comp(ld3(q.Q), i) : q.Q[i], Qj = SEL ? comp(ld3(q.Q), j) : q.Q[j];
+  const double vj = SEL ? comp(ld3(q.v), j) : q.v[j], ui = SEL ? comp(ld3(q.u), i) : q.u[i];
+  const double denom = nk * comp(r.d, k);
   // |denom| = inf: the full form's denom is NaN (0 * inf in the dot product)
   if (fabs(denom) < 1e-8 || fabs(denom) == kInf) return false;
-  const double tt = (q.D - q.n[k] * comp(r.o, k)) / denom;
+  const double tt = (q.D - nk * comp(r.o, k)) / denom;
   if (!(tmin <= tt && tt <= tmax)) return false;
-  const double pvi = (comp(r.o, i) + tt * comp(r.d, i)) - q.Q[i];
-  const double pvj = (comp(r.o, j) + tt * comp(r.d, j)) - q.Q[j];
-  const double ca = pvi * q.v[j], cb = q.u[i] * pvj;
+  const double pvi = (comp(r.o, i) + tt * comp(r.d, i)) - Qi;
+  const double pvj = (comp(r.o, j) + tt * comp(r.d, j)) - Qj;
+  const double ca = pvi * vj, cb = ui * pvj;
   const bool neg = (q.aa >> 6) & 1;
-  const double alpha = q.w[k] * (neg ? -ca : ca);
-  const double beta = q.w[k] * (neg ? -cb : cb);
+  const double alpha = wk * (neg ? -ca : ca);
+  const double beta = wk * (neg ? -cb : cb);
   if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) return false;
   t = tt;
   return true;
 }
+template <bool SEL = false>
 RT_HD RT_FI bool quad_t(const DQuad &q, const Ray &r, double tmin, double tmax,
                                        double &t) { // Plane.cpp:76-100
-  if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa(q, r, tmin, tmax, t);
+  if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa<SEL>(q, r, tmin, tmax, t);
   V3 n = ld3(q.n);
   double denom = dot(n, r.d);
   if (fabs(denom) < 1e-8) return false;
@@ -473,9 +507,10 @@ RT_HD RT_FI V3 rot_in(double s, double c, V3 p) {
 RT_HD RT_FI V3 rot_out(double s, double c, V3 p) {
   return v3((c * p.x) + (s * p.z), p.y, (-s * p.x) + (c * p.z));
 }
+template <bool U = false>
 RT_HD RT_FI Ray to_local(const DScene &S, int f, int n, Ray r) {
   for (int k = 0; k < n; ++k) {
-    const DXform X = S.xforms[f + k];
+    const DXform X = ldu<U>(S.xforms, f + k);
     if (X.kind == X_TRANSLATE) {
       r.o = r.o - v3(X.a, X.b, X.c);
     } else {
@@ -860,15 +895,60 @@ RT_HD RT_FI uint32_t wave_once() {
 #endif
 }
 
+// World items and spheres staged in LDS by the persistent instance (one
+// 16-wave block per CU owns the CU's LDS: C3's whole scene -- 485 nodes, 486
+// items, 486 spheres -- fits beside the traversal stacks).  items == nullptr:
+// nothing staged, every load goes to the scene tables in HBM / L2.
+struct LdsPrims {
+  const RT_LDS DItem *items;
+  const RT_LDS DSphere *spheres;
+};
+template <bool LP>
+RT_HD RT_FI DItem load_item(const DScene &S, const LdsPrims &lp, int i) {
+  if constexpr (LP) {
+    if (lp.items != nullptr) {
+      const RT_LDS DItem &L = lp.items[i];
+      DItem d;
+      d.kind = L.kind;
+      d.idx = L.idx;
+      d.xf_first = L.xf_first;
+      d.xf_count = L.xf_count;
+      d.mat = L.mat;
+      d.id = L.id;
+      d.pad[0] = d.pad[1] = 0;
+      return d;
+    }
+  }
+  return S.items[i];
+}
+template <bool LP>
+RT_HD RT_FI DSphere load_sphere(const DScene &S, const LdsPrims &lp, int i) {
+  if constexpr (LP) {
+    if (lp.items != nullptr) {
+      const RT_LDS DSphere &L = lp.spheres[i];
+      DSphere d;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        d.c0[k] = L.c0[k];
+        d.dir[k] = L.dir[k];
+      }
+      d.inv_r = L.inv_r;
+      d.rr = L.rr;
+      return d;
+    }
+  }
+  return S.spheres[i];
+}
+
 // The end of a closest-hit query: constant media tested against the final
 // primitive distance `closest` (the closest hit is the minimum over items in any
 // order, and a medium's free-flight draw is keyed by its id, not by visiting
 // order -- keeps the medium code out of the traversal loop's register budget),
 // then the hit record of the winning item, built once.
-template <bool STATS, unsigned F>
+template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &key,
                                            uint32_t bounce, double closest, int best,
-                                           Counters &cnt) {
+                                           Counters &cnt, const LdsPrims &lp = LdsPrims{}) {
   const double tmin = 0.001;
   constexpr bool kFlat = (F & F_FLAT) != 0;
   const bool moving = kFlat ? !S.static_spheres : true;
@@ -900,13 +980,13 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
   }
   if (best < 0) return false;
   if (!best_full) {
-    const DItem it = S.items[best];
+    const DItem it = load_item<LP>(S, lp, best);
     Ray lr = r;
     if constexpr ((F & F_XFORM) != 0) {
       if (it.xf_count) lr = to_local(S, it.xf_first, it.xf_count, r);
     }
     if (it.kind == I_SPHERE)
-      sphere_record(S.spheres[it.idx], lr, closest, it.mat, h, moving);
+      sphere_record(load_sphere<LP>(S, lp, it.idx), lr, closest, it.mat, h, moving);
     else
       quad_record(S.quads[it.idx], lr, closest, it.mat, h);
     if constexpr ((F & F_XFORM) != 0) {
@@ -922,10 +1002,11 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
 // traversal and build the hit record once at the end; media build theirs when hit.
 // `lnodes` is the LDS copy of nodes [0, S.n_lds_nodes) (the host emulator passes
 // S.nodes itself).
-template <bool STATS, unsigned F>
+template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                                       uint32_t bounce, int *stk, const RT_LDS DNode *lnodes,
-                                      Counters &cnt, RT_LDS LeafPool *pool = nullptr) {
+                                      Counters &cnt, RT_LDS LeafPool *pool = nullptr,
+                                      const LdsPrims &lp = LdsPrims{}) {
   const double tmin = 0.001; // Camera.cpp:242
   double closest = kInf;
   int best = -1;
@@ -947,15 +1028,17 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   }
   // hit test of world item ii against ray rr (|d|^2 = ra, its reciprocal ry)
   // in (tmin, tmax): the root in t
-  auto item_root = [&](int ii, const Ray &rr, double ra, double ry, double tmax,
-                       double &t) -> bool {
-    const DItem it = S.items[ii];
+  // (uniform: UTag<true> where ii is the same in every lane -- the flat walk)
+  auto item_root_t = [&](auto uniform, int ii, const Ray &rr, double ra, double ry, double tmax,
+                         double &t) -> bool {
+    constexpr bool U = decltype(uniform)::value && RT_UNIFORM_LOADS;
+    const DItem it = U ? ldu<U>(S.items, ii) : load_item<LP>(S, lp, ii);
     Ray lr = rr;
     double al = ra;
     bool local = false;
     if constexpr ((F & F_XFORM) != 0) {
       if (it.xf_count) {
-        lr = to_local(S, it.xf_first, it.xf_count, rr);
+        lr = to_local<U>(S, it.xf_first, it.xf_count, rr);
         al = len2(lr.d);
         local = true;
       }
@@ -965,16 +1048,22 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       // a local ray has its own |d|^2 and so its own reciprocal (a value, not
       // a pointer to one of two locals: that pointer kept ya in scratch memory)
       const double yl = local ? 1.0 / al : ry;
-      return sphere_root(S.spheres[it.idx], lr, al, tmin, tmax, t, moving, true, yl);
+      return sphere_root(U ? ldu<U>(S.spheres, it.idx) : load_sphere<LP>(S, lp, it.idx), lr, al,
+                         tmin, tmax, t, moving, true, yl);
     }
     if (STATS) cnt.quads++;
+    if constexpr (U) return quad_t<true>(ldu<true>(S.quads, it.idx), lr, tmin, tmax, t);
     return quad_t(S.quads[it.idx], lr, tmin, tmax, t);
   };
+  [[maybe_unused]] auto item_root = [&](int ii, const Ray &rr, double ra, double ry, double tmax,
+                                        double &t) -> bool {
+    return item_root_t(UTag<false>{}, ii, rr, ra, ry, tmax, t);
+  };
   // closest-hit test of one world item (records only t and the item index)
-  auto test_item = [&](int ii) {
+  auto test_item = [&](auto uniform, int ii) {
     if (STATS) cnt.wleaf += wave_once();
     double t;
-    const bool hit = item_root(ii, r, a, ya, closest, t);
+    const bool hit = item_root_t(uniform, ii, r, a, ya, closest, t);
     if (hit) {
       closest = t;
       if constexpr (kBoxes) cl32 = f32_up_c(closest);
@@ -1070,7 +1159,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
 
   if constexpr (kFlat) {
     // the reference's HittableList walk (HittableList.cpp), wave-uniform items
-    for (int ii = 0; ii < S.n_root_items; ++ii) test_item(ii);
+    for (int ii = 0; ii < S.n_root_items; ++ii) test_item(UTag<true>{}, ii);
   } else {
     // Speculative while-while traversal (Aila & Laine 2009, "postponed leaves"):
     // a lane that reaches its first leaf parks it in (lf, ln) and keeps walking
@@ -1217,7 +1306,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             const int ii = lf;
             ++lf;
             --ln;
-            test_item(ii);
+            test_item(UTag<false>{}, ii);
           }
         }
       } else
@@ -1228,7 +1317,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           const int ii = lf;
           ++lf;
           --ln;
-          test_item(ii);
+          test_item(UTag<false>{}, ii);
         }
       }
       if (cur < -1) { // a second leaf met while one was parked: it is next
@@ -1238,7 +1327,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       }
     }
   }
-  return trace_tail<STATS, F>(S, r, h, key, bounce, closest, best, cnt);
+  return trace_tail<STATS, F, LP>(S, r, h, key, bounce, closest, best, cnt, lp);
 }
 
 // ------------------------------------------------------------ lights
@@ -1541,13 +1630,14 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   return advance(ps, C);
 }
 
-template <bool STATS, unsigned F>
+template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
                                         const Key &key, int *stk, const RT_LDS DNode *lnodes,
-                                        Counters &cnt, RT_LDS LeafPool *pool = nullptr) {
+                                        Counters &cnt, RT_LDS LeafPool *pool = nullptr,
+                                        const LdsPrims &lp = LdsPrims{}) {
   Hit h;
   const uint64_t t0 = STATS ? clk() : 0;
-  const bool hit = trace<STATS, F>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt, pool);
+  const bool hit = trace<STATS, F, LP>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt, pool, lp);
   const uint64_t t1 = STATS ? clk() : 0;
   if (STATS && wave_once()) cnt.ctrace += t1 - t0;
   if (!hit) {

@@ -52,6 +52,16 @@ __global__ __launch_bounds__(256) void kern(unsigned long long *cycles, double *
       if constexpr (OP == 13) asm volatile("v_sqrt_f64 %0, %0" : "+v"(d[c]));
       if constexpr (OP == 14) asm volatile("v_floor_f64 %0, %0" : "+v"(d[c]));
       if constexpr (OP == 15) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[c]) : "v"(d[c]));
+      if constexpr (OP == 16) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(d[c]) : "v"(db), "v"(dc));
+      if constexpr (OP == 17) asm volatile("v_mov_b64 %0, %1" : "=v"(d[c]) : "v"(d[(c + 1) % CHAINS]));
+      if constexpr (OP == 18) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(*(unsigned *)&u[c]) : "v"(mb), "v"(mb));
+      if constexpr (OP == 19) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(*(unsigned *)&u[c]) : "v"(mb));
+      if constexpr (OP == 20) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f[c]) : "v"(fb));
+      if constexpr (OP == 21) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(f[c]) : "v"(fb));
+      if constexpr (OP == 22) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(u[c]) : "v"(u[(c + 1) % CHAINS]));
+      if constexpr (OP == 23) asm volatile("v_div_scale_f64 %0, vcc, %0, %1, %0" : "+v"(d[c]) : "v"(db) : "vcc");
+      if constexpr (OP == 24) asm volatile("v_div_fmas_f64 %0, %0, %1, %0" : "+v"(d[c]) : "v"(db));
+      if constexpr (OP == 25) asm volatile("v_ldexp_f64 %0, %0, 1" : "+v"(d[c]));
     }
   }
   unsigned long long t1 = __builtin_readcyclecounter();
@@ -112,5 +122,15 @@ int main() {
   run<12>("v_xor_b32", cus);
   run<6>("v_fma_f32", cus);
   run<7>("v_min3_f32", cus);
+  run<16>("v_pk_fma_f32", cus);
+  run<17>("v_mov_b64", cus);
+  run<18>("v_bitop3_b32", cus);
+  run<19>("v_mul_u32_u24", cus);
+  run<20>("v_mul_f32", cus);
+  run<21>("v_cndmask_b32", cus);
+  run<22>("v_lshl_add_u64", cus);
+  run<23>("v_div_scale_f64", cus);
+  run<24>("v_div_fmas_f64", cus);
+  run<25>("v_ldexp_f64", cus);
   return 0;
 }
