@@ -39,8 +39,8 @@ extern "C" hipError_t rtk_build_lbvh(const double *boxes, const DItem *items_in,
                                      DNode *nodes, DItem *items_out, int *depth_dev, void *temp,
                                      size_t temp_bytes, hipStream_t st);
 extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
-                                                const DLaunch *P, int n_chunks, double *out,
-                                                double *scratch, hipStream_t stream);
+                                                const DLaunch *P, int n_whole, int n_chunks,
+                                                double *out, double *scratch, hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double scale,
                                           uint8_t *bytes, hipStream_t stream);
 
@@ -163,6 +163,13 @@ int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
   L.chunk_strata = (L.sample_count + chunks - 1) / chunks;
   L.unit_ctr = nullptr;
   L.grid_cap = 0;
+  // one chunk: every tile is a whole unit; strata_chunks > 1 (tile layout):
+  // every tile split, its chunk partials are the caller's output (the launcher
+  // points parts at the output buffer)
+  L.n_whole = chunks > 1 ? 0 : L.n_local_tiles;
+  L.parts = nullptr;
+  L.parts_final = chunks > 1 ? 1 : 0;
+  L.pad_ = 0;
   return RT_OK;
 }
 
@@ -528,19 +535,47 @@ int rt_scene_destroy(rt_scene *s) {
   return RT_OK;
 }
 
-// Stratum chunks for a frame-layout launch over every tile: enough (tile,
-// chunk) work units for ~RTX_CHUNK_TARGET (default 32) per resident wave, so the
-// last round of waves is short (measured: C2 +3 %, C3 +8 %, C4 +6 %).
-static int frame_chunks(const rt_scene *s, const DLaunch &L) {
-  if (L.compact || L.tile_stride != 1 || L.tile_first != 0 || L.sample_count < 2) return 1;
+// Work units of a frame-layout launch over every tile (SplitPlan): the waves
+// should end together, so the launch must end on short units, while every
+// unit pays a refill-drain at its end (its last paths finish while lanes
+// idle), so units should be long.
+//  * Frames of more than 4 tiles per resident wave (1080p: 7.9 on 4,096 wave
+//    slots): the first tiles are whole units over all strata, written
+//    straight into the frame; the last `slots` tiles (RTX_TAIL_TILES per wave
+//    slot, default 1) are split into max(8, strata/32) stratum chunks -- the
+//    units the waves take last (dispatch / counter order), so the tail is a
+//    chunk, not a tile.
+//  * Smaller frames: every tile split, ~RTX_CHUNK_TARGET (default 32) units
+//    per wave slot (the round-1 rule).
+// RTX_CHUNK_TARGET=0: whole tiles only (tests).
+struct SplitPlan {
+  int n_whole, chunks;
+};
+static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
+  SplitPlan sp{L.n_local_tiles, 1};
+  if (L.compact || L.tile_stride != 1 || L.tile_first != 0 || L.sample_count < 2) return sp;
   int target = 32;
   if (const char *t = std::getenv("RTX_CHUNK_TARGET")) target = std::atoi(t);
-  if (target <= 0 || s->wave_slots <= 0) return 1;
-  const int64_t tiles = (int64_t)L.n_local_tiles;
-  int64_t c = ((int64_t)target * s->wave_slots + tiles - 1) / std::max<int64_t>(1, tiles);
-  c = std::max<int64_t>(1, std::min<int64_t>(c, L.sample_count));
-  const int64_t cs = (L.sample_count + c - 1) / c; // no empty chunks
-  return (int)((L.sample_count + cs - 1) / cs);
+  if (target <= 0 || s->wave_slots <= 0) return sp;
+  const int64_t tiles = (int64_t)L.n_local_tiles, slots = s->wave_slots;
+  auto no_empty = [&](int64_t c) { // no empty chunks
+    c = std::max<int64_t>(1, std::min<int64_t>(c, L.sample_count));
+    const int64_t cs = (L.sample_count + c - 1) / c;
+    return (int)((L.sample_count + cs - 1) / cs);
+  };
+  double tail = 1.0;
+  if (const char *t = std::getenv("RTX_TAIL_TILES")) tail = std::atof(t);
+  if (tiles > 4 * slots && tail > 0) {
+    const int64_t n_split = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
+    sp.chunks = no_empty(std::max<int64_t>(8, L.sample_count / 32));
+    sp.n_whole = (int)(tiles - n_split);
+    if (sp.chunks <= 1) sp.n_whole = L.n_local_tiles;
+    return sp;
+  }
+  const int64_t c = ((int64_t)target * slots + tiles - 1) / std::max<int64_t>(1, tiles);
+  sp.chunks = no_empty(c);
+  sp.n_whole = sp.chunks > 1 ? 0 : L.n_local_tiles;
+  return sp;
 }
 
 static int ensure_scratch(rt_scene *s, size_t bytes) {
@@ -557,11 +592,16 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
   return RT_OK;
 }
 
+// forced: the split plan of a tile-layout launch whose whole tiles go to
+// dev_out (compact) and split tiles' raw partials to the scene's scratch
+// (rt_multi_render's shards, reproducing the one-device frame's units)
 static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_out,
-                  unsigned long long *stats, hipStream_t st) {
-  const int chunks = stats ? 1 : frame_chunks(s, L);
-  if (chunks > 1) {
-    int rc = ensure_scratch(s, (size_t)L.n_local_tiles * chunks * 64 * 3 * sizeof(double));
+                  unsigned long long *stats, hipStream_t st, const SplitPlan *forced = nullptr) {
+  const SplitPlan sp = forced ? *forced : stats ? SplitPlan{L.n_local_tiles, 1} : frame_plan(s, L);
+  const bool split = !L.compact && sp.chunks > 1 && sp.n_whole < L.n_local_tiles;
+  if (split || forced) {
+    int rc = ensure_scratch(s, std::max<size_t>(1, (size_t)(L.n_local_tiles - sp.n_whole) * sp.chunks * 64 * 3) *
+                                   sizeof(double));
     if (rc) return rc;
   }
   // persistent waves pulling work units (RT_PERSISTENT=0 in the environment:
@@ -580,8 +620,17 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
-  e = chunks > 1 ? rtk_launch_render_chunked(&s->ds, &C, &Lp, chunks, dev_out, s->scratch, st)
-                 : rtk_launch_render(&s->ds, &C, &Lp, dev_out, stats, st);
+  if (forced) {
+    Lp.n_whole = sp.n_whole;
+    Lp.n_chunks = sp.chunks;
+    Lp.chunk_strata = (L.sample_count + sp.chunks - 1) / sp.chunks;
+    Lp.parts = s->scratch;
+    Lp.parts_final = 0;
+  } else if (L.parts_final) {
+    Lp.parts = dev_out; // tile layout, strata_chunks > 1: the chunk partials are the output
+  }
+  e = split ? rtk_launch_render_chunked(&s->ds, &C, &Lp, sp.n_whole, sp.chunks, dev_out, s->scratch, st)
+            : rtk_launch_render(&s->ds, &C, &Lp, dev_out, stats, st);
   if (e != hipSuccess) return hip_err(e, "render kernel launch");
   e = hipEventRecord(s->ev1, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
@@ -779,6 +828,48 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
   return RT_OK;
 }
 
+// One shard of rt_multi_render: the tiles t = first + k * stride in the tile
+// layout with the one-device frame's split plan -- tiles below plan.n_whole
+// (global index) as whole units, the rest in plan.chunks stratum chunks --
+// raw sums: the whole tiles' [k][64][3] into `whole`, the split tiles'
+// [k - whole tiles][chunk][64][3] into `parts` (host buffers, resized here).
+static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *p, int first,
+                        int stride, const SplitPlan &plan, int *n_whole_local,
+                        std::vector<double> &whole, std::vector<double> &parts) {
+  DCamera C;
+  DLaunch L;
+  rt_render_params q = *p;
+  q.tile_first = first;
+  q.tile_stride = stride;
+  q.layout = RT_LAYOUT_TILES;
+  q.strata_chunks = 0;
+  q.output = RT_OUT_SUM;
+  q.accumulate = 0;
+  int rc = to_device_camera(f, C);
+  if (rc) return rc;
+  if ((rc = to_launch(f, &q, L))) return rc;
+  SplitPlan sp = plan;
+  sp.n_whole = plan.n_whole > first ? std::min(L.n_local_tiles, (plan.n_whole - first + stride - 1) / stride) : 0;
+  *n_whole_local = sp.n_whole;
+  DeviceGuard g(s->device);
+  const size_t nw = (size_t)sp.n_whole * 64 * 3, np = (size_t)(L.n_local_tiles - sp.n_whole) * sp.chunks * 64 * 3;
+  try {
+    whole.resize(nw);
+    parts.resize(np);
+  } catch (const std::exception &) {
+    return set_err(RT_ERR_OOM, "host tile buffers");
+  }
+  if ((rc = ensure_out(s, std::max<size_t>(nw, 1) * sizeof(double)))) return rc;
+  if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream, &sp))) return rc;
+  hipError_t e = hipSuccess;
+  if (nw) e = hipMemcpyAsync(whole.data(), s->out_buf, nw * sizeof(double), hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess && np)
+    e = hipMemcpyAsync(parts.data(), s->scratch, np * sizeof(double), hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return hip_err(e, "shard render");
+  return RT_OK;
+}
+
 int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, double *host_rgb) {
   if (!m || !host_rgb || !p) return set_err(RT_ERR_INVALID, "null argument");
   if (p->tile_first != 0 || p->tile_stride > 1 || p->layout != RT_LAYOUT_FRAME)
@@ -792,35 +883,24 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   full.strata_chunks = 0;
   if ((rc = to_launch(f, &full, L))) return rc;
   const int n = (int)m->scenes.size();
-  int chunks = p->strata_chunks;
-  if (chunks <= 0) chunks = frame_chunks(m->scenes[0], L);
-  chunks = std::max(1, std::min(chunks, std::max(1, L.sample_count)));
+  // the one-device frame launch's units (so the frame is bit-identical to
+  // rt_render on one device), or every tile in strata_chunks chunks if asked
+  SplitPlan plan = frame_plan(m->scenes[0], L);
+  if (p->strata_chunks > 0) plan = SplitPlan{0, std::max(1, std::min(p->strata_chunks, std::max(1, L.sample_count)))};
+  if (plan.chunks <= 1) plan = SplitPlan{L.n_local_tiles, 1};
+  const int chunks = plan.chunks;
   const int W = f->image_width, r0 = L.row_begin, r1 = L.row_end;
   const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
-  std::vector<int> src(n, RT_OK);
+  std::vector<int> src(n, RT_OK), nwl(n, 0);
   std::vector<std::string> err(n);
+  std::vector<std::vector<double>> whole(n);
   std::vector<std::thread> th;
   try {
   for (int k = 0; k < n; ++k) {
     m->ms[k] = 0.0;
     if (k >= n_tiles) continue; // more shards than tiles
     th.emplace_back([&, k]() {
-      rt_render_params q = *p;
-      q.tile_first = k;
-      q.tile_stride = n;
-      q.layout = RT_LAYOUT_TILES;
-      q.strata_chunks = chunks;
-      q.output = RT_OUT_SUM;
-      q.accumulate = 0;
-      const int64_t local = (n_tiles - k + n - 1) / n;
-      try {
-        m->parts[k].resize((size_t)local * chunks * 64 * 3);
-      } catch (const std::exception &) {
-        src[k] = RT_ERR_OOM;
-        err[k] = "host tile buffer";
-        return;
-      }
-      src[k] = rt_render(m->scenes[k], f, &q, m->parts[k].data());
+      src[k] = render_shard(m->scenes[k], f, p, k, n, plan, &nwl[k], whole[k], m->parts[k]);
       if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
       if (src[k] != RT_OK) err[k] = g_err;
     });
@@ -832,20 +912,27 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   for (auto &t : th) t.join();
   for (int k = 0; k < n; ++k)
     if (src[k] != RT_OK) return set_err(src[k], "shard " + std::to_string(k) + ": " + err[k]);
-  // gather: tile t = k + lt*n of shard k; pixel (x, y) of the tile at slot y*8+x
+  // gather: tile t = k + lt*n of shard k; pixel (x, y) of the tile at slot
+  // y*8+x; a split tile's chunk partials added in chunk order (split_sum_kernel's)
   const bool scaled = p->output == RT_OUT_SCALED;
   for (int k = 0; k < n && k < n_tiles; ++k) {
-    const double *part = m->parts[k].data();
+    const double *wh = whole[k].data(), *part = m->parts[k].data();
     for (int64_t t = k, lt = 0; t < n_tiles; t += n, ++lt) {
       const int tx = (int)(t % L.tiles_x), ty = (int)(t / L.tiles_x);
+      const bool is_whole = lt < nwl[k];
       for (int slot = 0; slot < 64; ++slot) {
         const int i = tx * 8 + (slot & 7), j = r0 + ty * 8 + (slot >> 3);
         if (i >= W || j >= r1) continue;
         double *o = host_rgb + 3 * ((size_t)(j - r0) * W + i);
         for (int ch = 0; ch < 3; ++ch) {
-          const double *pp = part + ((size_t)lt * chunks * 64 + slot) * 3 + ch;
-          double sum = pp[0];
-          for (int c = 1; c < chunks; ++c) sum += pp[(size_t)c * 64 * 3];
+          double sum;
+          if (is_whole) {
+            sum = wh[((size_t)lt * 64 + slot) * 3 + ch];
+          } else {
+            const double *pp = part + ((size_t)(lt - nwl[k]) * chunks * 64 + slot) * 3 + ch;
+            sum = pp[0];
+            for (int c = 1; c < chunks; ++c) sum += pp[(size_t)c * 64 * 3];
+          }
           o[ch] = scaled ? C.scale * sum : sum;
         }
       }

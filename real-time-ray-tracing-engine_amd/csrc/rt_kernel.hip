@@ -120,13 +120,14 @@ struct KArgs {
 // on the GPU: tests/test_persistent.py, and through every BASELINE band).
 static_assert(sizeof(DScene) == 152 && alignof(DScene) == 8, "DScene kernarg layout");
 static_assert(sizeof(DCamera) == 208 && alignof(DCamera) == 8, "DCamera kernarg layout");
-static_assert(sizeof(DLaunch) == 80 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
+static_assert(sizeof(DLaunch) == 96 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
 static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 152 && offsetof(KArgs, P) == 360 &&
-                  offsetof(KArgs, out) == 440 && offsetof(KArgs, stats) == 448 &&
-                  sizeof(KArgs) == 456,
+                  offsetof(KArgs, out) == 456 && offsetof(KArgs, stats) == 464 &&
+                  sizeof(KArgs) == 472,
               "KArgs must mirror render_tiles' kernarg layout");
 static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
-                  offsetof(DLaunch, grid_cap) == 72,
+                  offsetof(DLaunch, grid_cap) == 72 && offsetof(DLaunch, n_whole) == 76 &&
+                  offsetof(DLaunch, parts) == 80 && offsetof(DLaunch, parts_final) == 88,
               "DLaunch field offsets read from the kernarg segment");
 template <bool FRESH>
 __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
@@ -153,6 +154,10 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
     L.chunk_strata = K.chunk_strata;
     L.unit_ctr = K.unit_ctr;
     L.grid_cap = K.grid_cap;
+    L.n_whole = K.n_whole;
+    L.parts = K.parts;
+    L.parts_final = K.parts_final;
+    L.pad_ = 0;
     return L;
   } else {
     return P;
@@ -253,10 +258,11 @@ __device__ __forceinline__ double *out_arg(double *out) {
   }
 }
 
-// PC ("persistent, chunked"): the instance for frame launches split into
-// stratum chunks (rtk_launch_render_chunked: tiles 0.., compact partials, plain
-// sums), whose waves persist and pull units; the launch fields those launches
-// fix are constants here, so they are not live across the path loop.
+// PC ("persistent, chunked"): the instance for frame launches over every tile
+// (rtk_launch_render_chunked: whole-tile units, then the stratum chunks of the
+// last tiles), whose waves persist and pull units; it reads the per-unit
+// launch fields afresh from the kernarg segment, so they are not live across
+// the path loop.
 template <bool STATS, unsigned F, bool PC = false>
 __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
   // the next ones come from the agent-scope counter (initialised by the host to
   // the grid's wave count), so waves take new units as they finish instead of
   // waiting for their block.
-  const int n_units = P.n_local_tiles * P.n_chunks;
+  const int n_units = P.n_whole + (P.n_local_tiles - P.n_whole) * P.n_chunks;
   int unit = blockIdx.x * BW + wv;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
   double *acc = &acc_lds[wv][0][0];
@@ -323,10 +329,19 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
-  const int local_tile = unit / PU.n_chunks, chunk = unit - local_tile * PU.n_chunks;
+  const bool whole = unit < PU.n_whole; // wave-uniform
+  int local_tile, s_first, s_count;
+  if (whole) {
+    local_tile = unit;
+    s_first = PU.sample_begin;
+    s_count = PU.sample_count;
+  } else {
+    const int u = unit - PU.n_whole, q = u / PU.n_chunks, chunk = u - q * PU.n_chunks;
+    local_tile = PU.n_whole + q;
+    s_first = PU.sample_begin + chunk * PU.chunk_strata;
+    s_count = min(PU.chunk_strata, PU.sample_count - chunk * PU.chunk_strata);
+  }
   const int tile = PC ? local_tile : PU.tile_first + local_tile * PU.tile_stride;
-  const int s_first = PU.sample_begin + chunk * PU.chunk_strata;
-  const int s_count = min(PU.chunk_strata, PU.sample_count - chunk * PU.chunk_strata);
   const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
   const int x0 = tx * 8, y0 = PU.row_begin + ty * 8;
   acc[lane * 3 + 0] = 0.0;
@@ -389,19 +404,25 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
   // ---- tile epilogue: one coalesced store per pixel
   {
     const DCamera Ce = camera_fields<kCamFresh>(C);
+    const DLaunch PE = launch_fields<PC && RT_KARG_FRESH>(P);
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
-    const bool compact = PC || P.compact;
-    if (compact || (i < Ce.W && j < P.row_end)) { // tile slots outside the image hold 0
+    // whole units: the frame (pixels outside the image are not written) or
+    // the compact tile layout; split units: their chunk's partial sums
+    const bool to_parts = !whole;
+    const bool compact = to_parts || PE.compact;
+    if (compact || (i < Ce.W && j < PE.row_end)) { // tile slots outside the image hold 0
       double sx = acc[lane * 3 + 0], sy = acc[lane * 3 + 1], sz = acc[lane * 3 + 2];
-      if (!PC && P.output == RT_OUT_SCALED) {
+      const bool final_out = !to_parts || PE.parts_final;
+      if (final_out && PE.output == RT_OUT_SCALED) {
         sx = Ce.scale * sx;
         sy = Ce.scale * sy;
         sz = Ce.scale * sz;
       }
       double *const ob = out_arg<PC && RT_KARG_FRESH>(out);
-      double *o = compact ? ob + 3 * ((size_t)unit * 64 + lane)
-                            : out + 3 * ((size_t)(j - P.row_begin) * Ce.W + i);
-      if (!PC && P.accumulate) {
+      double *o = to_parts ? PE.parts + 3 * ((size_t)(unit - PE.n_whole) * 64 + lane)
+                  : PE.compact ? ob + 3 * ((size_t)unit * 64 + lane)
+                               : ob + 3 * ((size_t)(j - PE.row_begin) * Ce.W + i);
+      if (final_out && PE.accumulate) {
         o[0] += sx;
         o[1] += sy;
         o[2] += sz;
@@ -436,23 +457,27 @@ __global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribu
   }
 }
 
-// Frame assembly after a chunked launch (rtk_launch_render_chunked): each
-// pixel's stratum-chunk partial sums, added in chunk order, become the frame
-// pixel (scaled / accumulated as the launch asks).
-__global__ void chunk_sum_kernel(const double *parts, DCamera C, DLaunch P, int n_chunks,
-                                 double *out) {
+// Frame assembly after a split launch (rtk_launch_render_chunked): each pixel
+// of the split tiles [n_whole, n_local_tiles) gets its stratum-chunk partial
+// sums added in chunk order (scaled / accumulated as the launch asks); the
+// whole tiles' pixels were written by their own units.  One thread per
+// (split tile, pixel slot, channel).
+__global__ void split_sum_kernel(const double *parts, DCamera C, DLaunch P, double *out) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int rows = P.row_end - P.row_begin;
-  if (idx >= (int64_t)C.W * rows * 3) return;
+  const int64_t n_split = P.n_local_tiles - P.n_whole;
+  if (idx >= n_split * 64 * 3) return;
   const int ch = (int)(idx % 3);
-  const int64_t pix = idx / 3;
-  const int i = (int)(pix % C.W), jr = (int)(pix / C.W);
-  const int tile = (jr >> 3) * P.tiles_x + (i >> 3), slot = ((jr & 7) << 3) | (i & 7);
-  const double *p = parts + ((size_t)tile * n_chunks * 64 + slot) * 3 + ch;
+  const int slot = (int)((idx / 3) & 63);
+  const int64_t st = idx / (64 * 3);
+  const int tile = P.n_whole + (int)st; // frame launches: tile_first 0, tile_stride 1
+  const int i = (tile % P.tiles_x) * 8 + (slot & 7), j = P.row_begin + (tile / P.tiles_x) * 8 + (slot >> 3);
+  if (i >= C.W || j >= P.row_end) return;
+  const double *p = parts + ((size_t)st * P.n_chunks * 64 + slot) * 3 + ch;
   double sum = p[0];
-  for (int k = 1; k < n_chunks; ++k) sum += p[(size_t)k * 64 * 3];
+  for (int k = 1; k < P.n_chunks; ++k) sum += p[(size_t)k * 64 * 3];
   if (P.output == RT_OUT_SCALED) sum = C.scale * sum;
-  out[idx] = P.accumulate ? out[idx] + sum : sum;
+  double *o = out + ((size_t)(j - P.row_begin) * C.W + i) * 3 + ch;
+  *o = P.accumulate ? *o + sum : sum;
 }
 
 __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint8_t *bytes) {
@@ -554,7 +579,7 @@ extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
-  const int64_t units = (int64_t)P->n_local_tiles * P->n_chunks;
+  const int64_t units = (int64_t)P->n_whole + (int64_t)(P->n_local_tiles - P->n_whole) * P->n_chunks;
   int blocks = (int)((units + kWaves - 1) / kWaves);
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
@@ -563,8 +588,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   DLaunch Q = *P;
   const unsigned f = (unsigned)(S->features & F_ALL);
   if (RT_PERSIST_F(f) && stats == nullptr && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
-      S->n_lds_nodes_pc >= 0 && units > (int64_t)Q.grid_cap * kPcWaves && Q.compact &&
-      Q.output == RT_OUT_SUM && !Q.accumulate && Q.tile_first == 0 && Q.tile_stride == 1) {
+      S->n_lds_nodes_pc >= 0 && units > (int64_t)Q.grid_cap * kPcWaves && !Q.compact &&
+      Q.tile_first == 0 && Q.tile_stride == 1) {
     // persistent: the resident blocks' waves take units [0, grid_cap * kPcWaves)
     // statically, the rest from the counter
     fn = persistent_instance(f);
@@ -585,24 +610,28 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   return hipGetLastError();
 }
 
-// Frame-layout launch split into (tile, stratum chunk) work units: finer units
-// shorten the tail of the last wave round; partials go to `scratch`
-// ([tiles][n_chunks][64][3]) and chunk_sum_kernel assembles the frame.
+// Frame-layout launch over every tile with its last tiles split: tiles
+// [0, n_whole) one work unit each, written straight into the frame; tiles
+// [n_whole, n_local_tiles) in n_chunks stratum chunks each -- the short units
+// the waves take last, so the launch ends on a short unit instead of a whole
+// tile -- whose partial sums go to `scratch` ([split tile][chunk][64][3]) and
+// split_sum_kernel adds them into the frame.
 extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
-                                                const DLaunch *P, int n_chunks, double *out,
-                                                double *scratch, hipStream_t stream) {
+                                                const DLaunch *P, int n_whole, int n_chunks,
+                                                double *out, double *scratch, hipStream_t stream) {
   DLaunch Q = *P;
-  Q.compact = 1;
-  Q.accumulate = 0;
-  Q.output = RT_OUT_SUM;
+  Q.compact = 0;
+  Q.n_whole = n_whole;
   Q.n_chunks = n_chunks;
   Q.chunk_strata = (P->sample_count + n_chunks - 1) / n_chunks;
-  hipError_t e = rtk_launch_render(S, C, &Q, scratch, nullptr, stream);
+  Q.parts = scratch;
+  Q.parts_final = 0;
+  hipError_t e = rtk_launch_render(S, C, &Q, out, nullptr, stream);
   if (e != hipSuccess) return e;
-  int64_t total = (int64_t)C->W * (P->row_end - P->row_begin) * 3;
-  if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL(chunk_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                     scratch, *C, *P, n_chunks, out);
+  const int64_t total = (int64_t)(Q.n_local_tiles - n_whole) * 64 * 3;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                     scratch, *C, Q, out);
   return hipGetLastError();
 }
 

@@ -445,6 +445,11 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
 #ifndef RT_UNIFORM_LOADS
 #define RT_UNIFORM_LOADS 1 // scalar loads of wave-uniform scene records (ldu)
 #endif
+// ... in the plain flat instance (C2 +2.7 %); the rich flat instances have no
+// SGPRs to spare for the records (C4 -1.6 %; profiles/r03d_ab.log)
+#ifndef RT_UNIFORM_LOADS_F
+#define RT_UNIFORM_LOADS_F(F) (RT_UNIFORM_LOADS != 0 && (F) == F_FLAT)
+#endif
 RT_HD RT_FI double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); } // no private array
 // SEL: the quad's axis components picked by value selects, not by an indexed
 // load -- for a record held in registers (a uniform scalar load, ldu), where
@@ -1031,7 +1036,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   // (uniform: UTag<true> where ii is the same in every lane -- the flat walk)
   auto item_root_t = [&](auto uniform, int ii, const Ray &rr, double ra, double ry, double tmax,
                          double &t) -> bool {
-    constexpr bool U = decltype(uniform)::value && RT_UNIFORM_LOADS;
+    constexpr bool U = decltype(uniform)::value && RT_UNIFORM_LOADS_F(F);
     const DItem it = U ? ldu<U>(S.items, ii) : load_item<LP>(S, lp, ii);
     Ray lr = rr;
     double al = ra;
