@@ -303,6 +303,8 @@ typedef struct rt_scene_info {
                                    scene's frames run one work unit per wavefront */
   int32_t lds_prims_persistent; /* 1: the persistent frame instance also stages every world
                                    item and sphere in LDS (whole tree staged and room left) */
+  int32_t persistent_block_waves; /* waves per block of the persistent instance: 16 (one block
+                                     per CU) or 4 (traversal stacks too deep for 16); 0: none */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

@@ -26,7 +26,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
 extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int64_t *free_bytes);
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes);
 extern "C" int rtk_lds_prims_enabled(void);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
 extern "C" size_t rtk_sah_temp_bytes(int n);
@@ -466,7 +466,9 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     // staged and room is left -- the world items and spheres (-1: no
     // persistent launches)
     int64_t pc_free = -1;
-    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pc_free);
+    int pcw = 0;
+    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pcw, &pc_free);
+    d.pc_waves = pcw;
     if (be != hipSuccess) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
@@ -511,6 +513,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.waves_per_simd = plan.waves_per_simd;
   in.lds_nodes_persistent = d.n_lds_nodes_pc;
   in.lds_prims_persistent = d.lds_items_pc > 0;
+  in.persistent_block_waves = d.pc_waves;
   *out = s;
   return RT_OK;
 }
@@ -613,7 +616,7 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   DLaunch Lp = L;
   if (persistent && s->wave_slots > 0) {
     Lp.unit_ctr = s->unit_ctr;
-    Lp.grid_cap = std::max(1, s->wave_slots / RT_PC_BLOCK_WAVES); // one persistent block per CU
+    Lp.grid_cap = std::max(1, s->wave_slots / std::max(1, s->ds.pc_waves)); // resident persistent blocks
     // RT_GRID_CAP: fewer resident blocks (tests: many units per wave)
     if (const char *g = getenv("RT_GRID_CAP"))
       if (atoi(g) > 0) Lp.grid_cap = atoi(g);

@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <array>
 #include <utility>
 
@@ -118,12 +119,12 @@ struct KArgs {
 // here instead of silently shifting what the persistent instance reads (its
 // frames are also checked bit for bit against the one-unit-per-wave instance
 // on the GPU: tests/test_persistent.py, and through every BASELINE band).
-static_assert(sizeof(DScene) == 152 && alignof(DScene) == 8, "DScene kernarg layout");
+static_assert(sizeof(DScene) == 160 && alignof(DScene) == 8, "DScene kernarg layout");
 static_assert(sizeof(DCamera) == 208 && alignof(DCamera) == 8, "DCamera kernarg layout");
 static_assert(sizeof(DLaunch) == 96 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
-static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 152 && offsetof(KArgs, P) == 360 &&
-                  offsetof(KArgs, out) == 456 && offsetof(KArgs, stats) == 464 &&
-                  sizeof(KArgs) == 472,
+static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 160 && offsetof(KArgs, P) == 368 &&
+                  offsetof(KArgs, out) == 464 && offsetof(KArgs, stats) == 472 &&
+                  sizeof(KArgs) == 480,
               "KArgs must mirror render_tiles' kernarg layout");
 static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
                   offsetof(DLaunch, grid_cap) == 72 && offsetof(DLaunch, n_whole) == 76 &&
@@ -242,6 +243,7 @@ __device__ __forceinline__ DScene scene_fields(const DScene &S) {
     D.n_lds_nodes_pc = K.n_lds_nodes_pc;
     D.lds_items_pc = K.lds_items_pc;
     D.lds_spheres_pc = K.lds_spheres_pc;
+    D.pc_waves = K.pc_waves;
     return D;
   } else {
     return S;
@@ -263,10 +265,14 @@ __device__ __forceinline__ double *out_arg(double *out) {
 // last tiles), whose waves persist and pull units; it reads the per-unit
 // launch fields afresh from the kernarg segment, so they are not live across
 // the path loop.
-template <bool STATS, unsigned F, bool PC = false>
-__global__ __launch_bounds__(64 * (PC ? RT_PC_WAVES : RT_BLOCK_WAVES)) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
+// PCW: 0 = one work unit per wavefront; else a persistent instance with
+// blocks of PCW waves (kPcWaves = one block per CU; kWaves when the traversal
+// stacks of 16 waves do not fit the CU's LDS, e.g. deep 4-wide trees)
+template <bool STATS, unsigned F, int PCW = 0>
+__global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
-  constexpr int BW = PC ? kPcWaves : kWaves; // waves per block
+  constexpr bool PC = PCW > 0;
+  constexpr int BW = PC ? PCW : kWaves; // waves per block
   constexpr bool kCamFresh = RT_CAM_FRESH_F(F);
   // the persistent instance stages its own (larger) node prefix
   DScene S = S_;
@@ -500,12 +506,14 @@ constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequen
   return {render_tiles<STATS, canonical(Fs)>...};
 }
 
-// the persistent chunked instances (RT_PERSIST_F feature sets)
-RenderFn persistent_instance(unsigned f) {
+// the persistent instances (RT_PERSIST_F feature sets), blocks of pcw waves
+RenderFn persistent_instance(unsigned f, int pcw) {
   if constexpr (RT_PERSIST_F(F_FLAT)) {
-    if (f == F_FLAT) return render_tiles<false, F_FLAT, true>;
+    if (f == F_FLAT) return pcw == kPcWaves ? render_tiles<false, F_FLAT, kPcWaves> : render_tiles<false, F_FLAT, kWaves>;
   }
-  return (f & F_BVH4) ? render_tiles<false, F_BVH4, true> : render_tiles<false, 0u, true>;
+  if (pcw == kPcWaves)
+    return (f & F_BVH4) ? render_tiles<false, F_BVH4, kPcWaves> : render_tiles<false, 0u, kPcWaves>;
+  return (f & F_BVH4) ? render_tiles<false, F_BVH4, kWaves> : render_tiles<false, 0u, kWaves>;
 }
 
 // one instance per feature set (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE | F_FLAT)
@@ -522,10 +530,10 @@ extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) 
   const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
   return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
-// the persistent instance's dynamic LDS (kPcWaves waves per block)
-static size_t lds_bytes_pc(int features, int stack_depth, int n_lds_nodes) {
+// a persistent instance's dynamic LDS (pcw waves per block)
+static size_t lds_bytes_pc(int features, int pcw, int stack_depth, int n_lds_nodes) {
   const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
-  return (size_t)kPcWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
+  return (size_t)pcw * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
 
 // LDS plan per block at the occupancy the instance's register count allows
@@ -557,21 +565,33 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   return hipSuccess;
 }
 
-// LDS the persistent instance (one kPcWaves-wave block per CU, which may own
-// the CU's whole LDS) has left for staging after its stacks and static LDS:
-// -1 when the stacks alone do not fit, or the feature set has no persistent
-// instance.
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int64_t *free_bytes) {
+// The persistent instance a scene uses and the LDS it has left for staging
+// after its stacks and static LDS: blocks of kPcWaves waves (one per CU, which
+// may own the CU's whole LDS) if their stacks fit, else blocks of kWaves waves
+// (one per SIMD at the occupancy target: a quarter of the CU's LDS each);
+// *pcw = 0 / *free_bytes = -1 when neither fits or the feature set has no
+// persistent instance.
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes) {
   *free_bytes = -1;
+  *pcw = 0;
   const unsigned f = (unsigned)(features & F_ALL);
   if (!RT_PERSIST_F(f)) return hipSuccess;
-  RenderFn fn = persistent_instance(f);
-  hipFuncAttributes a;
-  hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(fn));
-  if (e != hipSuccess) return e;
-  const size_t fixed = a.sharedSizeBytes + lds_bytes_pc(features, stack_depth, 0);
-  if (fixed > kLdsPerCu) return hipSuccess;
-  *free_bytes = (int64_t)(kLdsPerCu - fixed);
+  const char *force = getenv("RTX_PC_WAVES"); // tests: the 4-wave form on any scene
+  for (int w : {kPcWaves, kWaves}) {
+    if (force && atoi(force) == kWaves && w != kWaves) continue;
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(persistent_instance(f, w)));
+    if (e != hipSuccess) return e;
+    const int regs = ((a.numRegs + 7) / 8) * 8;
+    const int waves_per_simd = std::max(1, std::min(8, regs > 0 ? 512 / regs : 8));
+    const size_t per_block = kLdsPerCu / std::max(1, waves_per_simd * 4 / w);
+    const size_t fixed = a.sharedSizeBytes + lds_bytes_pc(features, w, stack_depth, 0);
+    if (fixed <= per_block) {
+      *pcw = w;
+      *free_bytes = (int64_t)(per_block - fixed);
+      return hipSuccess;
+    }
+  }
   return hipSuccess;
 }
 extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
@@ -588,20 +608,20 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   DLaunch Q = *P;
   const unsigned f = (unsigned)(S->features & F_ALL);
   if (RT_PERSIST_F(f) && stats == nullptr && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
-      S->n_lds_nodes_pc >= 0 && units > (int64_t)Q.grid_cap * kPcWaves && !Q.compact &&
+      S->pc_waves > 0 && units > (int64_t)Q.grid_cap * S->pc_waves && !Q.compact &&
       Q.tile_first == 0 && Q.tile_stride == 1) {
-    // persistent: the resident blocks' waves take units [0, grid_cap * kPcWaves)
+    // persistent: the resident blocks' waves take units [0, grid_cap * pc_waves)
     // statically, the rest from the counter
-    fn = persistent_instance(f);
+    fn = persistent_instance(f, S->pc_waves);
     blocks = Q.grid_cap;
-    block_waves = kPcWaves;
-    lds = lds_bytes_pc(S->features, S->stack_depth, S->n_lds_nodes_pc) +
+    block_waves = S->pc_waves;
+    lds = lds_bytes_pc(S->features, S->pc_waves, S->stack_depth, S->n_lds_nodes_pc) +
           (size_t)S->lds_items_pc * sizeof(DItem) + (size_t)S->lds_spheres_pc * sizeof(DSphere);
     // beyond 64 KB of LDS per block (set on every launch: cheap, and per device)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * kPcWaves, 1, stream);
+    e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * S->pc_waves, 1, stream);
     if (e != hipSuccess) return e;
   } else {
     Q.unit_ctr = nullptr; // every unit has its own wave

@@ -168,10 +168,11 @@ struct DScene {      // kernel argument (by value)
   int32_t stack_depth;   // per-lane traversal stack entries (BVH depth + 1)
   int32_t n_lds_nodes;   // nodes [0, n_lds_nodes) are staged in LDS (BFS order: top levels)
   int32_t static_spheres; // 1: every sphere has c1 == c0 (no motion blur): center = c0
-  int32_t n_lds_nodes_pc; // nodes staged by the persistent instance's one-per-CU blocks
-                          // (-1: its stacks do not fit, no persistent launches)
+  int32_t n_lds_nodes_pc; // nodes staged by the persistent instance's blocks (-1: none)
   int32_t lds_items_pc;   // world items [0, n) and spheres [0, lds_spheres_pc) the persistent
   int32_t lds_spheres_pc; // instance stages after its nodes (0: primitives stay in HBM)
+  int32_t pc_waves;       // waves per block of the persistent instance: RT_PC_WAVES (one
+                          // block per CU) or 4 (deep trees); 0: no persistent launches
 };
 
 // Scene features (kernel specialisation keys)

@@ -65,7 +65,8 @@ class SceneDesc(C.Structure):
                 ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
                 ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
-                ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32)]
+                ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32),
+                ("persistent_block_waves", C.c_int32)]
 
 
 RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
@@ -120,7 +121,8 @@ class SceneInfo(C.Structure):
                 ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
                 ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
-                ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32)]
+                ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32),
+                ("persistent_block_waves", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

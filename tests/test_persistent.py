@@ -32,14 +32,33 @@ def _render(S, f, seed, env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("name,arity,cap", [("bouncing_seed42", 2, 1), ("bouncing_seed42", 2, 3),
-                                            ("bouncing_seed42", 4, 2)])
-def test_persistent_waves_match_one_unit_per_wave(name, arity, cap):
+@pytest.mark.parametrize("name,arity,cap,pcw", [("bouncing_seed42", 2, 1, 16), ("bouncing_seed42", 2, 3, 16),
+                                                ("bouncing_seed42", 4, 2, 16), ("bouncing_seed42", 2, 3, 4),
+                                                ("bouncing_seed42", 4, 5, 4)])
+def test_persistent_waves_match_one_unit_per_wave(name, arity, cap, pcw):
+    """pcw: waves per persistent block -- 16 (one block per CU owning its LDS:
+    the whole tree, items and spheres staged) or 4 (the fallback for traversal
+    stacks too deep for 16 waves, forced here by RTX_PC_WAVES)."""
     S = load_scene(os.path.join(SCENES, name + ".json"))
     S.bvh_arity = arity
     cam = S.camera_desc(image_width=64, samples_per_pixel=16, max_depth=8)
     f = camera_frame(cam)
-    pers = _render(S, f, 5, {"RT_GRID_CAP": str(cap)})
+    env = {"RT_GRID_CAP": str(cap), "RTX_PC_WAVES": str(pcw)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with Renderer(S) as R:
+            info = R.info()
+            pers = R.render(f, seed=5)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert info["persistent_block_waves"] == pcw
+    if pcw == 16 and arity == 2:  # C3's scene: everything staged
+        assert info["lds_nodes_persistent"] == info["n_nodes"] and info["lds_prims_persistent"] == 1
     single = _render(S, f, 5, {"RT_GRID_CAP": "1000000"})  # cap above the block count: one unit per wave
     assert np.array_equal(pers, single)
     ref = O.oracle_render(S, cam, O.MODE_COUNTER, 5)
