@@ -39,8 +39,9 @@ extern "C" hipError_t rtk_build_lbvh(const double *boxes, const DItem *items_in,
                                      DNode *nodes, DItem *items_out, int *depth_dev, void *temp,
                                      size_t temp_bytes, hipStream_t st);
 extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
-                                                const DLaunch *P, int n_whole, int n_chunks,
-                                                double *out, double *scratch, hipStream_t stream);
+                                                const DLaunch *P, int n_head, int head_chunks,
+                                                int n_chunks, double *out, double *scratch,
+                                                hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double scale,
                                           uint8_t *bytes, hipStream_t stream);
 
@@ -166,10 +167,10 @@ int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
   // one chunk: every tile is a whole unit; strata_chunks > 1 (tile layout):
   // every tile split, its chunk partials are the caller's output (the launcher
   // points parts at the output buffer)
-  L.n_whole = chunks > 1 ? 0 : L.n_local_tiles;
+  L.n_head = chunks > 1 ? 0 : L.n_local_tiles;
+  L.head_chunks = 1;
   L.parts = nullptr;
   L.parts_final = chunks > 1 ? 1 : 0;
-  L.pad_ = 0;
   return RT_OK;
 }
 
@@ -540,44 +541,58 @@ int rt_scene_destroy(rt_scene *s) {
 
 // Work units of a frame-layout launch over every tile (SplitPlan): the waves
 // should end together, so the launch must end on short units, while every
-// unit pays a refill-drain at its end (its last paths finish while lanes
-// idle), so units should be long.
+// unit pays a refill drain at its end (its last paths finish while lanes
+// idle) and long units pay it less often.
 //  * Frames of more than 4 tiles per resident wave (1080p: 7.9 on 4,096 wave
-//    slots): the first tiles are whole units over all strata, written
-//    straight into the frame; the last `slots` tiles (RTX_TAIL_TILES per wave
-//    slot, default 1) are split into max(8, strata/32) stratum chunks -- the
-//    units the waves take last (dispatch / counter order), so the tail is a
-//    chunk, not a tile.
-//  * Smaller frames: every tile split, ~RTX_CHUNK_TARGET (default 32) units
-//    per wave slot (the round-1 rule).
+//    slots) with at most RTX_HEAD_STRATA (default 64) strata: whole tiles
+//    written straight into the frame, and the last `slots` x RTX_TAIL_TILES
+//    (default 0.5) tiles in 8 chunks each, the units the waves take last
+//    (dispatch / counter order), so the launch ends on a short unit (C2
+//    +4.5 % over every tile split; profiles/r03e_ab.log).  Head units of
+//    several chunks (more strata) are supported but measured slower than
+//    the uniform split below (C3 -9 % with whole 256-strata tiles, -1.5 %
+//    with a 2-slot tail), and their partials would grow with the strata.
+//  * Otherwise every tile split, ~RTX_CHUNK_TARGET (default 32) units per
+//    wave slot (the round-1 rule).
 // RTX_CHUNK_TARGET=0: whole tiles only (tests).
 struct SplitPlan {
-  int n_whole, chunks;
+  int n_head, head_chunks, chunks; // head tiles, their chunks; the tail tiles' chunks
 };
+static size_t plan_parts(const SplitPlan &sp, int n_local) { // chunk partial records
+  return (size_t)(sp.head_chunks > 1 ? (int64_t)sp.n_head * sp.head_chunks : 0) +
+         (size_t)(n_local - sp.n_head) * (sp.n_head < n_local ? sp.chunks : 0);
+}
 static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
-  SplitPlan sp{L.n_local_tiles, 1};
+  SplitPlan sp{L.n_local_tiles, 1, 1};
   if (L.compact || L.tile_stride != 1 || L.tile_first != 0 || L.sample_count < 2) return sp;
   int target = 32;
   if (const char *t = std::getenv("RTX_CHUNK_TARGET")) target = std::atoi(t);
   if (target <= 0 || s->wave_slots <= 0) return sp;
   const int64_t tiles = (int64_t)L.n_local_tiles, slots = s->wave_slots;
-  auto no_empty = [&](int64_t c) { // no empty chunks
+  auto no_empty = [&](int64_t c) { // chunk count with no empty chunks
     c = std::max<int64_t>(1, std::min<int64_t>(c, L.sample_count));
     const int64_t cs = (L.sample_count + c - 1) / c;
     return (int)((L.sample_count + cs - 1) / cs);
   };
-  double tail = 1.0;
+  double tail = 0.5;
   if (const char *t = std::getenv("RTX_TAIL_TILES")) tail = std::atof(t);
-  if (tiles > 4 * slots && tail > 0) {
-    const int64_t n_split = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
-    sp.chunks = no_empty(std::max<int64_t>(8, L.sample_count / 32));
-    sp.n_whole = (int)(tiles - n_split);
-    if (sp.chunks <= 1) sp.n_whole = L.n_local_tiles;
+  int head_max = 64;
+  if (const char *h = std::getenv("RTX_HEAD_STRATA")) head_max = std::max(1, std::atoi(h));
+  const int64_t head_chunks = (L.sample_count + head_max - 1) / head_max;
+  // partial records of a head/tail plan: bounded by 4 frames (a tail of
+  // chunked tiles + head chunks); otherwise the uniform split
+  const bool bounded = head_chunks == 1 || head_chunks * tiles <= 4 * tiles;
+  if (tiles > 4 * slots && tail > 0 && bounded) {
+    const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
+    sp.head_chunks = no_empty((L.sample_count + head_max - 1) / head_max);
+    sp.chunks = no_empty(8 * (int64_t)sp.head_chunks);
+    sp.n_head = (int)(tiles - n_tail);
+    if (sp.chunks <= 1) sp = SplitPlan{L.n_local_tiles, 1, 1};
     return sp;
   }
   const int64_t c = ((int64_t)target * slots + tiles - 1) / std::max<int64_t>(1, tiles);
   sp.chunks = no_empty(c);
-  sp.n_whole = sp.chunks > 1 ? 0 : L.n_local_tiles;
+  if (sp.chunks > 1) sp.n_head = 0;
   return sp;
 }
 
@@ -600,11 +615,11 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
 // (rt_multi_render's shards, reproducing the one-device frame's units)
 static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_out,
                   unsigned long long *stats, hipStream_t st, const SplitPlan *forced = nullptr) {
-  const SplitPlan sp = forced ? *forced : stats ? SplitPlan{L.n_local_tiles, 1} : frame_plan(s, L);
-  const bool split = !L.compact && sp.chunks > 1 && sp.n_whole < L.n_local_tiles;
+  const SplitPlan sp = forced ? *forced : stats ? SplitPlan{L.n_local_tiles, 1, 1} : frame_plan(s, L);
+  const size_t n_parts = plan_parts(sp, L.n_local_tiles);
+  const bool split = !L.compact && n_parts > 0;
   if (split || forced) {
-    int rc = ensure_scratch(s, std::max<size_t>(1, (size_t)(L.n_local_tiles - sp.n_whole) * sp.chunks * 64 * 3) *
-                                   sizeof(double));
+    int rc = ensure_scratch(s, std::max<size_t>(1, n_parts * 64 * 3) * sizeof(double));
     if (rc) return rc;
   }
   // persistent waves pulling work units (RT_PERSISTENT=0 in the environment:
@@ -624,7 +639,8 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   if (forced) {
-    Lp.n_whole = sp.n_whole;
+    Lp.n_head = sp.n_head;
+    Lp.head_chunks = sp.head_chunks;
     Lp.n_chunks = sp.chunks;
     Lp.chunk_strata = (L.sample_count + sp.chunks - 1) / sp.chunks;
     Lp.parts = s->scratch;
@@ -632,7 +648,8 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   } else if (L.parts_final) {
     Lp.parts = dev_out; // tile layout, strata_chunks > 1: the chunk partials are the output
   }
-  e = split ? rtk_launch_render_chunked(&s->ds, &C, &Lp, sp.n_whole, sp.chunks, dev_out, s->scratch, st)
+  e = split ? rtk_launch_render_chunked(&s->ds, &C, &Lp, sp.n_head, sp.head_chunks, sp.chunks, dev_out,
+                                        s->scratch, st)
             : rtk_launch_render(&s->ds, &C, &Lp, dev_out, stats, st);
   if (e != hipSuccess) return hip_err(e, "render kernel launch");
   e = hipEventRecord(s->ev1, st);
@@ -832,12 +849,12 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
 }
 
 // One shard of rt_multi_render: the tiles t = first + k * stride in the tile
-// layout with the one-device frame's split plan -- tiles below plan.n_whole
-// (global index) as whole units, the rest in plan.chunks stratum chunks --
-// raw sums: the whole tiles' [k][64][3] into `whole`, the split tiles'
-// [k - whole tiles][chunk][64][3] into `parts` (host buffers, resized here).
+// layout with the one-device frame's split plan -- tiles below plan.n_head
+// (global index) as head units, the rest as tail chunks -- raw sums: whole
+// head tiles' [k][64][3] into `whole`, the chunk partials (the launch's parts
+// layout) into `parts` (host buffers, resized here).
 static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *p, int first,
-                        int stride, const SplitPlan &plan, int *n_whole_local,
+                        int stride, const SplitPlan &plan, SplitPlan *local,
                         std::vector<double> &whole, std::vector<double> &parts) {
   DCamera C;
   DLaunch L;
@@ -852,10 +869,11 @@ static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *
   if (rc) return rc;
   if ((rc = to_launch(f, &q, L))) return rc;
   SplitPlan sp = plan;
-  sp.n_whole = plan.n_whole > first ? std::min(L.n_local_tiles, (plan.n_whole - first + stride - 1) / stride) : 0;
-  *n_whole_local = sp.n_whole;
+  sp.n_head = plan.n_head > first ? std::min(L.n_local_tiles, (plan.n_head - first + stride - 1) / stride) : 0;
+  *local = sp;
   DeviceGuard g(s->device);
-  const size_t nw = (size_t)sp.n_whole * 64 * 3, np = (size_t)(L.n_local_tiles - sp.n_whole) * sp.chunks * 64 * 3;
+  const size_t nw = sp.head_chunks == 1 ? (size_t)sp.n_head * 64 * 3 : 0;
+  const size_t np = plan_parts(sp, L.n_local_tiles) * 64 * 3;
   try {
     whole.resize(nw);
     parts.resize(np);
@@ -889,12 +907,12 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   // the one-device frame launch's units (so the frame is bit-identical to
   // rt_render on one device), or every tile in strata_chunks chunks if asked
   SplitPlan plan = frame_plan(m->scenes[0], L);
-  if (p->strata_chunks > 0) plan = SplitPlan{0, std::max(1, std::min(p->strata_chunks, std::max(1, L.sample_count)))};
-  if (plan.chunks <= 1) plan = SplitPlan{L.n_local_tiles, 1};
-  const int chunks = plan.chunks;
+  if (p->strata_chunks > 0)
+    plan = SplitPlan{0, 1, std::max(1, std::min(p->strata_chunks, std::max(1, L.sample_count)))};
   const int W = f->image_width, r0 = L.row_begin, r1 = L.row_end;
   const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
-  std::vector<int> src(n, RT_OK), nwl(n, 0);
+  std::vector<int> src(n, RT_OK);
+  std::vector<SplitPlan> lp(n, plan);
   std::vector<std::string> err(n);
   std::vector<std::vector<double>> whole(n);
   std::vector<std::thread> th;
@@ -903,7 +921,7 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
     m->ms[k] = 0.0;
     if (k >= n_tiles) continue; // more shards than tiles
     th.emplace_back([&, k]() {
-      src[k] = render_shard(m->scenes[k], f, p, k, n, plan, &nwl[k], whole[k], m->parts[k]);
+      src[k] = render_shard(m->scenes[k], f, p, k, n, plan, &lp[k], whole[k], m->parts[k]);
       if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
       if (src[k] != RT_OK) err[k] = g_err;
     });
@@ -916,13 +934,18 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   for (int k = 0; k < n; ++k)
     if (src[k] != RT_OK) return set_err(src[k], "shard " + std::to_string(k) + ": " + err[k]);
   // gather: tile t = k + lt*n of shard k; pixel (x, y) of the tile at slot
-  // y*8+x; a split tile's chunk partials added in chunk order (split_sum_kernel's)
+  // y*8+x; a chunked tile's partials added in chunk order (split_sum_kernel's)
   const bool scaled = p->output == RT_OUT_SCALED;
   for (int k = 0; k < n && k < n_tiles; ++k) {
+    const SplitPlan &sp = lp[k];
     const double *wh = whole[k].data(), *part = m->parts[k].data();
     for (int64_t t = k, lt = 0; t < n_tiles; t += n, ++lt) {
       const int tx = (int)(t % L.tiles_x), ty = (int)(t / L.tiles_x);
-      const bool is_whole = lt < nwl[k];
+      const bool head = lt < sp.n_head, is_whole = head && sp.head_chunks == 1;
+      const int nc = head ? sp.head_chunks : sp.chunks;
+      const int64_t part0 = head ? lt * nc
+                                 : (sp.head_chunks > 1 ? (int64_t)sp.n_head * sp.head_chunks : 0) +
+                                       (lt - sp.n_head) * nc;
       for (int slot = 0; slot < 64; ++slot) {
         const int i = tx * 8 + (slot & 7), j = r0 + ty * 8 + (slot >> 3);
         if (i >= W || j >= r1) continue;
@@ -932,9 +955,9 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
           if (is_whole) {
             sum = wh[((size_t)lt * 64 + slot) * 3 + ch];
           } else {
-            const double *pp = part + ((size_t)(lt - nwl[k]) * chunks * 64 + slot) * 3 + ch;
+            const double *pp = part + ((size_t)part0 * 64 + slot) * 3 + ch;
             sum = pp[0];
-            for (int c = 1; c < chunks; ++c) sum += pp[(size_t)c * 64 * 3];
+            for (int c = 1; c < nc; ++c) sum += pp[(size_t)c * 64 * 3];
           }
           o[ch] = scaled ? C.scale * sum : sum;
         }

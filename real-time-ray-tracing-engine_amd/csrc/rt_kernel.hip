@@ -127,8 +127,9 @@ static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 160 && offsetof(K
                   sizeof(KArgs) == 480,
               "KArgs must mirror render_tiles' kernarg layout");
 static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
-                  offsetof(DLaunch, grid_cap) == 72 && offsetof(DLaunch, n_whole) == 76 &&
-                  offsetof(DLaunch, parts) == 80 && offsetof(DLaunch, parts_final) == 88,
+                  offsetof(DLaunch, grid_cap) == 72 && offsetof(DLaunch, n_head) == 76 &&
+                  offsetof(DLaunch, parts) == 80 && offsetof(DLaunch, parts_final) == 88 &&
+                  offsetof(DLaunch, head_chunks) == 92,
               "DLaunch field offsets read from the kernarg segment");
 template <bool FRESH>
 __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
@@ -155,10 +156,10 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
     L.chunk_strata = K.chunk_strata;
     L.unit_ctr = K.unit_ctr;
     L.grid_cap = K.grid_cap;
-    L.n_whole = K.n_whole;
+    L.n_head = K.n_head;
     L.parts = K.parts;
     L.parts_final = K.parts_final;
-    L.pad_ = 0;
+    L.head_chunks = K.head_chunks;
     return L;
   } else {
     return P;
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((a
   // the next ones come from the agent-scope counter (initialised by the host to
   // the grid's wave count), so waves take new units as they finish instead of
   // waiting for their block.
-  const int n_units = P.n_whole + (P.n_local_tiles - P.n_whole) * P.n_chunks;
+  const int n_units = P.n_head * P.head_chunks + (P.n_local_tiles - P.n_head) * P.n_chunks;
   int unit = blockIdx.x * BW + wv;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
   double *acc = &acc_lds[wv][0][0];
@@ -335,17 +336,19 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((a
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
   const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
-  const bool whole = unit < PU.n_whole; // wave-uniform
+  // (wave-uniform) head unit: tile unit / head_chunks; tail unit: a chunk of
+  // the tail tile n_head + (unit - head units) / n_chunks
+  const int head_units = PU.n_head * PU.head_chunks;
+  const bool whole = PU.head_chunks == 1 && unit < PU.n_head;
   int local_tile, s_first, s_count;
-  if (whole) {
-    local_tile = unit;
-    s_first = PU.sample_begin;
-    s_count = PU.sample_count;
-  } else {
-    const int u = unit - PU.n_whole, q = u / PU.n_chunks, chunk = u - q * PU.n_chunks;
-    local_tile = PU.n_whole + q;
-    s_first = PU.sample_begin + chunk * PU.chunk_strata;
-    s_count = min(PU.chunk_strata, PU.sample_count - chunk * PU.chunk_strata);
+  {
+    const bool head = unit < head_units;
+    const int nc = head ? PU.head_chunks : PU.n_chunks;
+    const int cs = head ? (PU.sample_count + nc - 1) / nc : PU.chunk_strata;
+    const int u = head ? unit : unit - head_units, q = u / nc, chunk = u - q * nc;
+    local_tile = head ? q : PU.n_head + q;
+    s_first = PU.sample_begin + chunk * cs;
+    s_count = min(cs, PU.sample_count - chunk * cs);
   }
   const int tile = PC ? local_tile : PU.tile_first + local_tile * PU.tile_stride;
   const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
@@ -425,7 +428,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((a
         sz = Ce.scale * sz;
       }
       double *const ob = out_arg<PC && RT_KARG_FRESH>(out);
-      double *o = to_parts ? PE.parts + 3 * ((size_t)(unit - PE.n_whole) * 64 + lane)
+      const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
+      double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
                   : PE.compact ? ob + 3 * ((size_t)unit * 64 + lane)
                                : ob + 3 * ((size_t)(j - PE.row_begin) * Ce.W + i);
       if (final_out && PE.accumulate) {
@@ -464,23 +468,28 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((a
 }
 
 // Frame assembly after a split launch (rtk_launch_render_chunked): each pixel
-// of the split tiles [n_whole, n_local_tiles) gets its stratum-chunk partial
-// sums added in chunk order (scaled / accumulated as the launch asks); the
-// whole tiles' pixels were written by their own units.  One thread per
-// (split tile, pixel slot, channel).
+// of a chunked tile gets its stratum-chunk partial sums added in chunk order
+// (scaled / accumulated as the launch asks) -- the head tiles' head_chunks
+// partials when head_chunks > 1, the tail tiles' n_chunks partials; whole
+// tiles' pixels were written by their own units.  One thread per (chunked
+// tile, pixel slot, channel).
 __global__ void split_sum_kernel(const double *parts, DCamera C, DLaunch P, double *out) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n_split = P.n_local_tiles - P.n_whole;
-  if (idx >= n_split * 64 * 3) return;
+  const int first = P.head_chunks > 1 ? 0 : P.n_head; // first chunked tile
+  if (idx >= (int64_t)(P.n_local_tiles - first) * 64 * 3) return;
   const int ch = (int)(idx % 3);
   const int slot = (int)((idx / 3) & 63);
-  const int64_t st = idx / (64 * 3);
-  const int tile = P.n_whole + (int)st; // frame launches: tile_first 0, tile_stride 1
+  const int tile = first + (int)(idx / (64 * 3)); // frame launches: tile_first 0, tile_stride 1
   const int i = (tile % P.tiles_x) * 8 + (slot & 7), j = P.row_begin + (tile / P.tiles_x) * 8 + (slot >> 3);
   if (i >= C.W || j >= P.row_end) return;
-  const double *p = parts + ((size_t)st * P.n_chunks * 64 + slot) * 3 + ch;
+  const bool head = tile < P.n_head;
+  const int nc = head ? P.head_chunks : P.n_chunks;
+  const int64_t part0 = head ? (int64_t)tile * nc
+                             : (P.head_chunks > 1 ? (int64_t)P.n_head * P.head_chunks : 0) +
+                                   (int64_t)(tile - P.n_head) * nc;
+  const double *p = parts + (part0 * 64 + slot) * 3 + ch;
   double sum = p[0];
-  for (int k = 1; k < P.n_chunks; ++k) sum += p[(size_t)k * 64 * 3];
+  for (int k = 1; k < nc; ++k) sum += p[(size_t)k * 64 * 3];
   if (P.output == RT_OUT_SCALED) sum = C.scale * sum;
   double *o = out + ((size_t)(j - P.row_begin) * C.W + i) * 3 + ch;
   *o = P.accumulate ? *o + sum : sum;
@@ -599,7 +608,7 @@ extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
-  const int64_t units = (int64_t)P->n_whole + (int64_t)(P->n_local_tiles - P->n_whole) * P->n_chunks;
+  const int64_t units = (int64_t)P->n_head * P->head_chunks + (int64_t)(P->n_local_tiles - P->n_head) * P->n_chunks;
   int blocks = (int)((units + kWaves - 1) / kWaves);
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
@@ -630,25 +639,28 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   return hipGetLastError();
 }
 
-// Frame-layout launch over every tile with its last tiles split: tiles
-// [0, n_whole) one work unit each, written straight into the frame; tiles
-// [n_whole, n_local_tiles) in n_chunks stratum chunks each -- the short units
-// the waves take last, so the launch ends on a short unit instead of a whole
-// tile -- whose partial sums go to `scratch` ([split tile][chunk][64][3]) and
-// split_sum_kernel adds them into the frame.
+// Frame-layout launch over every tile in the host's split plan (rt_api.cpp
+// frame_plan): head tiles [0, n_head) in head_chunks units each (1: whole
+// units written straight into the frame), then the tail tiles in n_chunks
+// finer units -- the units the waves take last, so the launch ends on short
+// units; chunk partials go to `scratch` and split_sum_kernel adds them into
+// the frame.
 extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *C,
-                                                const DLaunch *P, int n_whole, int n_chunks,
-                                                double *out, double *scratch, hipStream_t stream) {
+                                                const DLaunch *P, int n_head, int head_chunks,
+                                                int n_chunks, double *out, double *scratch,
+                                                hipStream_t stream) {
   DLaunch Q = *P;
   Q.compact = 0;
-  Q.n_whole = n_whole;
+  Q.n_head = n_head;
+  Q.head_chunks = head_chunks;
   Q.n_chunks = n_chunks;
   Q.chunk_strata = (P->sample_count + n_chunks - 1) / n_chunks;
   Q.parts = scratch;
   Q.parts_final = 0;
   hipError_t e = rtk_launch_render(S, C, &Q, out, nullptr, stream);
   if (e != hipSuccess) return e;
-  const int64_t total = (int64_t)(Q.n_local_tiles - n_whole) * 64 * 3;
+  const int first = head_chunks > 1 ? 0 : n_head;
+  const int64_t total = (int64_t)(Q.n_local_tiles - first) * 64 * 3;
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                      scratch, *C, Q, out);

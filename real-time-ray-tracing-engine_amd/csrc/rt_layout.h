@@ -210,20 +210,21 @@ struct DLaunch {
   int32_t tile_first, tile_stride; // tiles rendered: tile_first + k * tile_stride
   int32_t n_local_tiles;           // k in [0, n_local_tiles)
   int32_t compact;                 // RT_LAYOUT_TILES output
-  // Work units: local tiles [0, n_whole) are one unit each over all launched
-  // strata ("whole" units: their pixels are final -- frame or compact tile
-  // layout, scaled / accumulated as asked); tiles [n_whole, n_local_tiles) are
-  // split into n_chunks units of chunk_strata strata each, whose per-pixel
-  // partial sums go to parts[(tile - n_whole) * n_chunks + chunk][64][3]
-  // (raw sums for a frame launch -- split_sum_kernel adds them in chunk order;
-  // the caller's output when parts_final: RT_LAYOUT_TILES with strata_chunks).
+  // Work units: the head tiles [0, n_head) in head_chunks stratum chunks each
+  // (head_chunks 1: "whole" units whose pixels are final -- frame or compact
+  // tile layout, scaled / accumulated as asked); the tail tiles [n_head,
+  // n_local_tiles) in n_chunks chunks of chunk_strata strata each.  Chunk units
+  // write per-pixel partial sums to parts[u'][64][3], u' = unit when
+  // head_chunks > 1, else unit - n_head (raw sums for a frame launch --
+  // split_sum_kernel adds them in chunk order; the caller's output when
+  // parts_final: RT_LAYOUT_TILES with strata_chunks).
   int32_t n_chunks, chunk_strata;
   int32_t *unit_ctr;               // persistent launch: next work unit (device counter), or null
   int32_t grid_cap;                // persistent launch: resident blocks of the instance (0: none)
-  int32_t n_whole;
+  int32_t n_head;
   double *parts;
   int32_t parts_final;
-  int32_t pad_;
+  int32_t head_chunks;
 };
 
 #endif

@@ -105,3 +105,30 @@ def test_cli_gpus_shards_ppm_byte_identical(tmp_path):
         outs[tag] = (tmp_path / "output" / (tag + ".ppm")).read_bytes()
     assert outs["one"].startswith(b"P3\n64 64\n255\n")
     assert outs["two"] == outs["one"] and outs["five"] == outs["one"]
+
+
+# Frames of more than 4 tiles per resident wave take the head/tail plan
+# (rt_api.cpp frame_plan): whole head tiles (<= 64 strata) or head tiles in a
+# few chunks, the last tiles in 8x finer chunks.  rt_multi_render reproduces
+# the plan per shard, so the frame stays bit-identical; the plan only changes
+# the fp64 summation grouping against the uniform split (RTX_TAIL_TILES=0).
+PLAN_CASES = [("three_spheres.json", 4), ("bouncing_seed42.json", 100)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,spp", PLAN_CASES, ids=[c[0] for c in PLAN_CASES])
+def test_multi_render_head_tail_plan_bit_identical(scene, spp):
+    S = load_scene(os.path.join(SCENES, scene))
+    f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=spp, max_depth=6))
+    with Renderer(S, device=0) as R:
+        one = R.render(f, seed=4)
+        os.environ["RTX_TAIL_TILES"] = "0"
+        try:
+            uniform = R.render(f, seed=4)
+        finally:
+            del os.environ["RTX_TAIL_TILES"]
+    np.testing.assert_allclose(one, uniform, rtol=1e-12, atol=1e-14)
+    for shards in (2, 3):
+        with MultiRenderer(S, devices=(0,), shards=shards) as M:
+            got = M.render(f, seed=4)
+        assert np.array_equal(got, one), (shards, np.abs(got - one).max())
