@@ -790,7 +790,7 @@ int rt_to_bytes_device(const double *rgb, int64_t n, double scale, uint8_t *byte
 // One rt_scene per shard, one host thread per shard (StaticCamera::render_gpu's
 // single-device loop, StaticCamera.cpp:136-313, spread over N devices).  Shard
 // k renders tiles k, k+N, k+2N, ... in the compact tile layout; the host adds
-// each pixel's chunk partials in chunk order -- the order chunk_sum_kernel
+// each pixel's chunk partials in chunk order -- the order split_sum_kernel
 // uses -- so with the frame launch's chunk split the frame is bit-identical to
 // rt_render on one device.
 struct rt_multi {

@@ -11,7 +11,7 @@ spp 4096, depth 8 -- 129,600 8x8 tiles, 33.97 G samples per frame.
       row split (top + bottom half) reassembles it (pixel and stratum indexing,
       the Philox keys of a 4K frame, the per-launch chunk counts);
     - the chunked frame launch (work units = (tile, stratum chunk), partials in
-      the scratch buffer, chunk_sum_kernel) equals the one-unit-per-tile launch
+      the scratch buffer, split_sum_kernel) equals the one-unit-per-tile launch
       (no scratch) up to fp64 summation order -- the scratch / chunk sizing at
       129,600 tiles;
     - every channel finite, the image not black;

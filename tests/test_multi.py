@@ -5,7 +5,7 @@
 
 With the frame launch's stratum-chunk split (strata_chunks 0) each (tile, chunk)
 work unit traces exactly the samples it traces in the one-device frame launch,
-and the host adds the chunk partials in chunk_sum_kernel's order, so the
+and the host adds the chunk partials in split_sum_kernel's order, so the
 sharded frame is bit-identical to rt_render on one device -- checked with
 np.array_equal and on the CLI's PPM bytes.  Virtual shards (K > N) put several
 shards on the one GPU of the test box."""
