@@ -53,6 +53,16 @@ using namespace rtp;
 #define RT_BLOCK_WAVES 4
 #endif
 constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
+// Flat instances (no BVH, nothing staged in LDS) run one-wave blocks: a
+// block's wave slots are released only when all of its waves have ended, so
+// with 4-wave blocks a slot idles until the slowest unit of its block is done
+// (measured: C2 +2.0 %, C4 +10.4 % over 4-wave blocks; 2-wave blocks +0.5 % /
+// +6.3 %; profiles/r03g_ab.log).  BVH instances keep 4-wave blocks: their
+// waves share the block's staged BVH prefix.
+#ifndef RT_FLAT_BLOCK_WAVES
+#define RT_FLAT_BLOCK_WAVES 1
+#endif
+constexpr int block_waves(unsigned f) { return (f & F_FLAT) ? RT_FLAT_BLOCK_WAVES : RT_BLOCK_WAVES; }
 // Waves per block of the persistent instance: one block per CU (16 = 4 SIMDs x
 // its 4-waves/SIMD target), so the CU's 160 KB of LDS holds ONE copy of the
 // staged BVH beside its 16 waves' stacks instead of four copies for four
@@ -261,19 +271,19 @@ __device__ __forceinline__ double *out_arg(double *out) {
   }
 }
 
-// PC ("persistent, chunked"): the instance for frame launches over every tile
-// (rtk_launch_render_chunked: whole-tile units, then the stratum chunks of the
-// last tiles), whose waves persist and pull units; it reads the per-unit
-// launch fields afresh from the kernarg segment, so they are not live across
-// the path loop.
+// PC (persistent): the instance for launches of more units than the grid's
+// resident waves -- frame launches (head units, then the tail chunks) and
+// tile-subset launches (multi-GPU shards) alike -- whose waves persist and
+// pull units; it reads the per-unit launch fields afresh from the kernarg
+// segment, so they are not live across the path loop.
 // PCW: 0 = one work unit per wavefront; else a persistent instance with
 // blocks of PCW waves (kPcWaves = one block per CU; kWaves when the traversal
 // stacks of 16 waves do not fit the CU's LDS, e.g. deep 4-wide trees)
 template <bool STATS, unsigned F, int PCW = 0>
-__global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   constexpr bool PC = PCW > 0;
-  constexpr int BW = PC ? PCW : kWaves; // waves per block
+  constexpr int BW = PC ? PCW : block_waves(F); // waves per block
   constexpr bool kCamFresh = RT_CAM_FRESH_F(F);
   // the persistent instance stages its own (larger) node prefix
   DScene S = S_;
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : RT_BLOCK_WAVES)) __attribute__((a
     s_first = PU.sample_begin + chunk * cs;
     s_count = min(cs, PU.sample_count - chunk * cs);
   }
-  const int tile = PC ? local_tile : PU.tile_first + local_tile * PU.tile_stride;
+  const int tile = PU.tile_first + local_tile * PU.tile_stride;
   const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
   const int x0 = tx * 8, y0 = PU.row_begin + ty * 8;
   acc[lane * 3 + 0] = 0.0;
@@ -537,7 +547,8 @@ const RenderFn *render_table(bool stats) {
 // ---------------------------------------------------------------- launchers
 extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) {
   const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
-  return (size_t)kWaves * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
+  return (size_t)block_waves((unsigned)features) * stack_depth * 64 * sizeof(int) +
+         (size_t)n_lds_nodes * node;
 }
 // a persistent instance's dynamic LDS (pcw waves per block)
 static size_t lds_bytes_pc(int features, int pcw, int stack_depth, int n_lds_nodes) {
@@ -561,7 +572,8 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
   if (const char *c = getenv("RTX_LDS_CAP"))
     if (atoi(c) > 0 && (size_t)atoi(c) < cap) cap = (size_t)atoi(c);
-  const int blocks_per_cu = waves_per_simd * 4 / kWaves > 0 ? waves_per_simd * 4 / kWaves : 1;
+  const int bw = block_waves((unsigned)features);
+  const int blocks_per_cu = waves_per_simd * 4 / bw > 0 ? waves_per_simd * 4 / bw : 1;
   size_t per_block = lds_cu / blocks_per_cu;
   if (per_block > cap) per_block = cap;
   const size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(features, stack_depth, 0);
@@ -609,21 +621,21 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
   const int64_t units = (int64_t)P->n_head * P->head_chunks + (int64_t)(P->n_local_tiles - P->n_head) * P->n_chunks;
-  int blocks = (int)((units + kWaves - 1) / kWaves);
+  const int bw = block_waves((unsigned)S->features);
+  int blocks = (int)((units + bw - 1) / bw);
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
   size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
-  int block_waves = kWaves;
+  int launch_waves = bw;
   DLaunch Q = *P;
   const unsigned f = (unsigned)(S->features & F_ALL);
   if (RT_PERSIST_F(f) && stats == nullptr && Q.unit_ctr != nullptr && Q.grid_cap > 0 &&
-      S->pc_waves > 0 && units > (int64_t)Q.grid_cap * S->pc_waves && !Q.compact &&
-      Q.tile_first == 0 && Q.tile_stride == 1) {
+      S->pc_waves > 0 && units > (int64_t)Q.grid_cap * S->pc_waves) {
     // persistent: the resident blocks' waves take units [0, grid_cap * pc_waves)
     // statically, the rest from the counter
     fn = persistent_instance(f, S->pc_waves);
     blocks = Q.grid_cap;
-    block_waves = S->pc_waves;
+    launch_waves = S->pc_waves;
     lds = lds_bytes_pc(S->features, S->pc_waves, S->stack_depth, S->n_lds_nodes_pc) +
           (size_t)S->lds_items_pc * sizeof(DItem) + (size_t)S->lds_spheres_pc * sizeof(DSphere);
     // beyond 64 KB of LDS per block (set on every launch: cheap, and per device)
@@ -635,7 +647,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   } else {
     Q.unit_ctr = nullptr; // every unit has its own wave
   }
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * block_waves), lds, stream, *S, *C, Q, out, stats);
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * launch_waves), lds, stream, *S, *C, Q, out, stats);
   return hipGetLastError();
 }
 

@@ -473,6 +473,9 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
 #ifndef RT_UNIFORM_LOADS
 #define RT_UNIFORM_LOADS 1 // scalar loads of wave-uniform scene records (ldu)
 #endif
+#ifndef RT_STACK_GUARD
+#define RT_STACK_GUARD 0 // traversal stack overflow check per push (trace)
+#endif
 // ... in the plain flat instance (C2 +2.7 %); the rich flat instances have no
 // SGPRs to spare for the records (C4 -1.6 %; profiles/r03d_ab.log)
 #ifndef RT_UNIFORM_LOADS_F
@@ -1203,7 +1206,26 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     // inner node, -1 none (stack empty: done after the parked leaf), <= -2 a leaf
     // ~(first << 3 | count) (count >= 1).  Visiting order only changes how much
     // the closest-hit bound culls, never the closest hit.
-    int sp = 0;
+    // The stack as a pointer to the next free entry (stk[64 k]: this lane's
+    // k-th entry): a push is a store and one add, a pop one add and a load --
+    // no sp * 256 address arithmetic per access.  No overflow guard: the host
+    // sizes S.stack_depth to what the walk can push -- one entry per level of
+    // the binary tree (a pushed entry is the sibling of a node on the current
+    // root path), three per 4-wide level -- plus one, from the depth of the
+    // tree it built (RT_STACK_GUARD=1 restores the per-push check).
+    int *top = stk;
+    auto push = [&](int e) {
+#if RT_STACK_GUARD
+      if (top == stk + 64 * S.stack_depth) return;
+#endif
+      *top = e;
+      top += 64;
+    };
+    auto pop = [&]() -> int {
+      if (top == stk) return -1;
+      top -= 64;
+      return *top;
+    };
     int cur;
     int lf = 0, ln = 0;
     if (S.root_is_leaf) {
@@ -1263,12 +1285,12 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           cswap(1, 2);
 #pragma unroll
           for (int c = 3; c >= 1; --c)
-            if (tn[c] != __builtin_huge_valf() && sp < S.stack_depth) stk[64 * sp++] = en[c];
-          cur = tn[0] != __builtin_huge_valf() ? en[0] : (sp > 0 ? stk[64 * --sp] : -1);
+            if (tn[c] != __builtin_huge_valf()) push(en[c]);
+          cur = tn[0] != __builtin_huge_valf() ? en[0] : pop();
           if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
             lf = (~cur) >> 3;
             ln = (~cur) & 7;
-            cur = sp > 0 ? stk[64 * --sp] : -1;
+            cur = pop();
           }
         }
       } else
@@ -1303,17 +1325,17 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         const int e0 = N.entry[0], e1 = N.entry[1];
         if (h0 && h1) {
           const bool first0 = tn0 <= tn1;
-          if (sp < S.stack_depth) stk[64 * sp++] = first0 ? e1 : e0;
+          push(first0 ? e1 : e0);
           cur = first0 ? e0 : e1;
         } else if (h0 || h1) {
           cur = h0 ? e0 : e1;
         } else {
-          cur = sp > 0 ? stk[64 * --sp] : -1;
+          cur = pop();
         }
         if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
           lf = (~cur) >> 3;
           ln = (~cur) & 7;
-          cur = sp > 0 ? stk[64 * --sp] : -1;
+          cur = pop();
         }
       }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1356,7 +1378,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       if (cur < -1) { // a second leaf met while one was parked: it is next
         lf = (~cur) >> 3;
         ln = (~cur) & 7;
-        cur = sp > 0 ? stk[64 * --sp] : -1;
+        cur = pop();
       }
     }
   }

@@ -63,3 +63,31 @@ def test_persistent_waves_match_one_unit_per_wave(name, arity, cap, pcw):
     assert np.array_equal(pers, single)
     ref = O.oracle_render(S, cam, O.MODE_COUNTER, 5)
     assert np.abs(pers - ref).max() <= 1e-4
+
+
+@pytest.mark.parametrize("layout_chunks", [1, 4])
+def test_persistent_tile_subset_launch(layout_chunks):
+    """Tile-subset launches (a multi-GPU rank's tiles t = 1 (mod 3), compact
+    RT_LAYOUT_TILES output, optionally stratum chunks) also run persistent when
+    they have more units than resident waves: bit-identical to one unit per
+    wave."""
+    from rtx import abi
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    cam = S.camera_desc(image_width=64, samples_per_pixel=16, max_depth=8)
+    f = camera_frame(cam)
+
+    def run(cap):
+        old = os.environ.get("RT_GRID_CAP")
+        os.environ["RT_GRID_CAP"] = str(cap)
+        try:
+            with Renderer(S) as R:
+                return R.render(f, seed=8, output=abi.RT_OUT_SUM, tiles=(1, 3),
+                                layout=abi.RT_LAYOUT_TILES, chunks=layout_chunks)
+        finally:
+            if old is None:
+                os.environ.pop("RT_GRID_CAP")
+            else:
+                os.environ["RT_GRID_CAP"] = old
+    pers, single = run(1), run(1000000)
+    assert np.array_equal(pers, single)
+    assert pers.any()
