@@ -309,7 +309,7 @@ RT_HD RT_FI double sin_n(double x) {
 // branches on it, it only scales the albedo), so the host build (emulator)
 // keeps the reference's order and images agree with the oracle to ~1e-15.
 #ifndef RT_PERLIN_LERP
-#define RT_PERLIN_LERP 0 // C4 +6.6 % with 4-wave blocks, +0.1 % with the one-wave blocks (r03g, r03h): reference order kept
+#define RT_PERLIN_LERP 1 // C4 +6.6 % (4-wave blocks, r03g) and +5.3 % (one-wave blocks: r03h 3,207 vs r03j 3,047)
 #endif
 RT_HD double perlin_noise(const DPerlin &P, V3 p) {
   double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
