@@ -166,10 +166,9 @@ __global__ void emit_nodes(int n, const int *left, const int *right, const doubl
   const int ch[2] = {left[i], right[i]};
   for (int k = 0; k < 2; ++k) {
     const double *b = child_box(ch[k], leaf_box, node_box);
-    float *lo = k ? d.lo1 : d.lo0, *hi = k ? d.hi1 : d.hi0;
     for (int q = 0; q < 3; ++q) {
-      lo[q] = f32_lo(b[q]);
-      hi[q] = f32_hi(b[q + 3]);
+      d.lo[q][k] = f32_lo(b[q]);
+      d.hi[q][k] = f32_hi(b[q + 3]);
     }
     d.entry[k] = ch[k] >= 0 ? ch[k] : ~(((~ch[k]) << 3) | 1);
   }

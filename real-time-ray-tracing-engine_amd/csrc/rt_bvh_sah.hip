@@ -339,10 +339,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void sah_apply(
   if (lane == 0) {
     DNode n;
     for (int q = 0; q < 3; ++q) {
-      n.lo0[q] = llo[q];
-      n.hi0[q] = lhi[q];
-      n.lo1[q] = rlo[q];
-      n.hi1[q] = rhi[q];
+      n.lo[q][0] = llo[q];
+      n.hi[q][0] = lhi[q];
+      n.lo[q][1] = rlo[q];
+      n.hi[q][1] = rhi[q];
     }
     n.entry[0] = n.entry[1] = -1; // written by the children at the next level
     n.pad[0] = n.pad[1] = 0;

@@ -88,12 +88,13 @@ struct DMedium {     // ConstantMedium: -1/density, phase material, boundary ite
 };
 
 struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + links
-  float lo0[3], hi0[3];
-  float lo1[3], hi1[3];
+  float lo[3][2];    // lo[axis][child]: the two children's planes of one axis side by
+  float hi[3][2];    // side, so one packed fp32 FMA (v_pk_fma_f32) computes both
   int32_t entry[2];  // >= 0: inner node index; < 0: leaf ~((first << 3) | count),
                      // items [first, first + count) (items are stored in leaf order)
   int32_t pad[2];
 };
+static_assert(sizeof(DNode) == 64, "DNode layout");
 
 // 4-wide BVH node (128 B): the boxes of up to four children in SoA order
 // (lo x[4], lo y[4], lo z[4], hi x[4], ...), fp32 rounded outward like DNode's,

@@ -867,6 +867,64 @@ RT_HD RT_FI bool slab_hit(const RayF<true> &q, const float *lo, const float *hi,
 #endif
   return tl <= fmaf(th, kSlabGrow, q.slack);
 }
+// Both children of a binary node (slab_hit each).  RT_SLAB_PK (device): the
+// twelve plane FMAs as six packed fp32 FMAs (v_pk_fma_f32, full rate) on the
+// child-interleaved planes lo[axis][child] -- the same IEEE fma per element,
+// so the same entry distances and verdicts as twelve scalar fmaf.
+#ifndef RT_SLAB_PK
+#define RT_SLAB_PK 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef float rt_f2 __attribute__((ext_vector_type(2)));
+#endif
+RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, float cl32, float &t0,
+                           float &t1, bool &h0, bool &h1) {
+#if defined(__HIP_DEVICE_COMPILE__) && RT_SLAB_PK
+  // the six per-ray constants in three register pairs (1/d_x, 1/d_y), (1/d_z,
+  // -p_x), (-p_y, -p_z), broadcast into both halves by op_sel -- the splat
+  // pairs the compiler builds otherwise take six more VGPRs across the walk
+  const rt_f2 k0 = {q.inv[0], q.inv[1]}, k1 = {q.inv[2], -q.p[0]}, k2 = {-q.p[1], -q.p[2]};
+  rt_f2 a[3], b[3];
+  const rt_f2 lx = {N.lo[0][0], N.lo[0][1]}, hx = {N.hi[0][0], N.hi[0][1]};
+  const rt_f2 ly = {N.lo[1][0], N.lo[1][1]}, hy = {N.hi[1][0], N.hi[1][1]};
+  const rt_f2 lz = {N.lo[2][0], N.lo[2][1]}, hz = {N.hi[2][0], N.hi[2][1]};
+  // x: k0.lo * plane + k1.hi;  y: k0.hi * plane + k2.lo;  z: k1.lo * plane + k2.hi
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(a[0]) : "v"(lx), "v"(k0), "v"(k1));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(b[0]) : "v"(hx), "v"(k0), "v"(k1));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(a[1]) : "v"(ly), "v"(k0), "v"(k2));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(b[1]) : "v"(hy), "v"(k0), "v"(k2));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(a[2]) : "v"(lz), "v"(k1), "v"(k2));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(b[2]) : "v"(hz), "v"(k1), "v"(k2));
+  // entry / exit distances in asm too: the packed FMAs' results come out of
+  // asm, which the compiler cannot prove canonical, so fminf / fmaxf would
+  // re-canonicalise each of them (one v_max per plane distance)
+  auto verdict = [&](float a0, float b0, float a1, float b1, float a2, float b2, float &tl) {
+    float n0, n1, n2, f0, f1, f2, th;
+    asm("v_min_f32 %[n0], %[a0], %[b0]\n\t"
+        "v_min_f32 %[n1], %[a1], %[b1]\n\t"
+        "v_min_f32 %[n2], %[a2], %[b2]\n\t"
+        "v_max_f32 %[n2], %[n2], %[tmin]\n\t"
+        "v_max3_f32 %[tl], %[n0], %[n1], %[n2]\n\t"
+        "v_max_f32 %[f0], %[a0], %[b0]\n\t"
+        "v_max_f32 %[f1], %[a1], %[b1]\n\t"
+        "v_max_f32 %[f2], %[a2], %[b2]\n\t"
+        "v_min3_f32 %[f2], %[f2], %[cl], %[f1]\n\t"
+        "v_min_f32 %[th], %[f0], %[f2]"
+        : [tl] "=&v"(tl), [th] "=&v"(th), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2),
+          [f0] "=&v"(f0), [f1] "=&v"(f1), [f2] "=&v"(f2)
+        : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1), [a2] "v"(a2), [b2] "v"(b2),
+          [tmin] "s"(tmin32), [cl] "v"(cl32));
+    return tl <= fmaf(th, kSlabGrow, q.slack);
+  };
+  h0 = verdict(a[0].x, b[0].x, a[1].x, b[1].x, a[2].x, b[2].x, t0);
+  h1 = verdict(a[0].y, b[0].y, a[1].y, b[1].y, a[2].y, b[2].y, t1);
+#else
+  const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
+  const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
+  h0 = slab_hit(q, lo0, hi0, tmin32, cl32, t0);
+  h1 = slab_hit(q, lo1, hi1, tmin32, cl32, t1);
+#endif
+}
 // f32_up(x) as a canonical float (the min/max operations take it as is
 // instead of re-canonicalising it at every box test)
 RT_HD RT_FI float f32_up_c(double x) {
@@ -1302,12 +1360,12 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         if (cur < S.n_lds_nodes) {
           const RT_LDS DNode &L = lnodes[cur];
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            N.lo0[k] = L.lo0[k];
-            N.hi0[k] = L.hi0[k];
-            N.lo1[k] = L.lo1[k];
-            N.hi1[k] = L.hi1[k];
-          }
+          for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              N.lo[a][k] = L.lo[a][k];
+              N.hi[a][k] = L.hi[a][k];
+            }
           N.entry[0] = L.entry[0];
           N.entry[1] = L.entry[1];
         } else {
@@ -1315,11 +1373,13 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
         }
 #if RT_SLAB_FMA
         float tn0, tn1;
-        const bool h0 = slab_hit(q, N.lo0, N.hi0, tmin32, cl32, tn0);
-        const bool h1 = slab_hit(q, N.lo1, N.hi1, tmin32, cl32, tn1);
+        bool h0, h1;
+        slab_hit2(q, N, tmin32, cl32, tn0, tn1, h0, h1);
 #else
-        const float tn0 = slab(q, N.lo0, N.hi0, tmin32, cl32);
-        const float tn1 = slab(q, N.lo1, N.hi1, tmin32, cl32);
+        const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
+        const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
+        const float tn0 = slab(q, lo0, hi0, tmin32, cl32);
+        const float tn1 = slab(q, lo1, hi1, tmin32, cl32);
         const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
 #endif
         const int e0 = N.entry[0], e1 = N.entry[1];

@@ -307,10 +307,9 @@ struct SahBuilder {
       int ch[2] = {p.left, p.right};
       for (int k = 0; k < 2; ++k) {
         const BNode &c = bn[ch[k]];
-        float *lo = k ? d.lo1 : d.lo0, *hi = k ? d.hi1 : d.hi0;
         for (int a = 0; a < 3; ++a) {
-          lo[a] = f32_lo(c.b.lo[a]);
-          hi[a] = f32_hi(c.b.hi[a]);
+          d.lo[a][k] = f32_lo(c.b.lo[a]);
+          d.hi[a][k] = f32_hi(c.b.hi[a]);
         }
         d.entry[k] = c.left < 0 ? ~((c.first << 3) | c.count) : map[ch[k]];
       }
@@ -986,8 +985,8 @@ double bvh_sah_cost(const std::vector<DNode> &nodes) {
   };
   float rlo[3], rhi[3];
   for (int a = 0; a < 3; ++a) {
-    rlo[a] = std::min(nodes[0].lo0[a], nodes[0].lo1[a]);
-    rhi[a] = std::max(nodes[0].hi0[a], nodes[0].hi1[a]);
+    rlo[a] = std::min(nodes[0].lo[a][0], nodes[0].lo[a][1]);
+    rhi[a] = std::max(nodes[0].hi[a][0], nodes[0].hi[a][1]);
   }
   const double root = area(rlo, rhi);
   if (!(root > 0.0)) return 0.0;
@@ -996,7 +995,9 @@ double bvh_sah_cost(const std::vector<DNode> &nodes) {
     for (int k = 0; k < 2; ++k) {
       const int e = d.entry[k];
       const double w = e >= 0 ? 1.0 : (double)((~e) & 7);
-      c += w * area(k ? d.lo1 : d.lo0, k ? d.hi1 : d.hi0) / root;
+      const float lo[3] = {d.lo[0][k], d.lo[1][k], d.lo[2][k]};
+      const float hi[3] = {d.hi[0][k], d.hi[1][k], d.hi[2][k]};
+      c += w * area(lo, hi) / root;
     }
   return c;
 }
@@ -1011,8 +1012,8 @@ int collapse_bvh4(const std::vector<DNode> &bin, std::vector<DNode4> &out) {
   auto child = [&](const DNode &b, int k) {
     Child c;
     for (int a = 0; a < 3; ++a) {
-      c.lo[a] = k ? b.lo1[a] : b.lo0[a];
-      c.hi[a] = k ? b.hi1[a] : b.hi0[a];
+      c.lo[a] = b.lo[a][k];
+      c.hi[a] = b.hi[a][k];
     }
     c.e = b.entry[k];
     return c;

@@ -169,8 +169,8 @@ extern "C" int emu_bvh4_info(const rt_scene_desc *desc, long long *info) {
   // every child box of a 4-wide node is a child box of some binary node
   std::vector<std::array<float, 6>> bb;
   for (const DNode &n : H.nodes) {
-    bb.push_back({n.lo0[0], n.lo0[1], n.lo0[2], n.hi0[0], n.hi0[1], n.hi0[2]});
-    bb.push_back({n.lo1[0], n.lo1[1], n.lo1[2], n.hi1[0], n.hi1[1], n.hi1[2]});
+    bb.push_back({n.lo[0][0], n.lo[1][0], n.lo[2][0], n.hi[0][0], n.hi[1][0], n.hi[2][0]});
+    bb.push_back({n.lo[0][1], n.lo[1][1], n.lo[2][1], n.hi[0][1], n.hi[1][1], n.hi[2][1]});
   }
   std::sort(bb.begin(), bb.end());
   long long foreign = 0;

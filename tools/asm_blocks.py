@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Basic blocks of one render_tiles<STATS, F> instance in the gfx950 asm
 (make asm): instruction counts by class for the blocks that look like the BVH
-walk (fp32 FMAs / LDS reads).   python tools/asm_blocks.py F [--pc] [--all] [--dump BB]"""
+walk (fp32 FMAs / LDS reads).   python tools/asm_blocks.py F [--pc (the 16-wave persistent instance)] [--all] [--dump BB]"""
 import re
 import sys
 
@@ -10,7 +10,7 @@ ASM = "real-time-ray-tracing-engine_amd/build/asm/rt_kernel-hip-amdgcn-amd-amdhs
 
 def blocks(F, stats=0, pc=0):
     s = open(ASM).read()
-    name = "_ZN12_GLOBAL__N_112render_tilesILb%dELj%dELb%dEEEv6DScene7DCamera7DLaunchPdPy" % (stats, F, pc)
+    name = "_ZN12_GLOBAL__N_112render_tilesILb%dELj%dELi%dEEEv6DScene7DCamera7DLaunchPdPy" % (stats, F, pc)
     i = s.index(name + ":")
     j = s.index(".Lfunc_end", i)
     out, cur = [], ["entry", []]
@@ -39,7 +39,7 @@ def classify(ins):
 
 if __name__ == "__main__":
     F = int(sys.argv[1])
-    bl = blocks(F, pc=int("--pc" in sys.argv))
+    bl = blocks(F, pc=16 if "--pc" in sys.argv else 0)
     if "--dump" in sys.argv:
         want = sys.argv[sys.argv.index("--dump") + 1]
         for b, ins in bl:
