@@ -872,7 +872,7 @@ RT_HD RT_FI bool slab_hit(const RayF<true> &q, const float *lo, const float *hi,
 // child-interleaved planes lo[axis][child] -- the same IEEE fma per element,
 // so the same entry distances and verdicts as twelve scalar fmaf.
 #ifndef RT_SLAB_PK
-#define RT_SLAB_PK 1
+#define RT_SLAB_PK 0 // measured C3 -2.1 %: 3 more spilled VGPRs outweigh 5 VALU per visit (profiles/r03k_ab.log)
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef float rt_f2 __attribute__((ext_vector_type(2)));
