@@ -184,7 +184,10 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
 #define RT_CAM_FRESH 0 // measured: C4 -17 % (every segment), -21 % (regeneration only); profiles/r03b_ab.log, r03c_ab.log
 #endif
 #ifndef RT_EPI_FRESH
-#define RT_EPI_FRESH 1
+#define RT_EPI_FRESH 1 // non-flat instances only: the flat one measured -0.5 % kernel time with it (C2; C4 neutral); profiles/r03l_ab.log
+#endif
+#ifndef RT_EPI_FRESH_F
+#define RT_EPI_FRESH_F(F) (RT_EPI_FRESH != 0 && ((F) & F_FLAT) == 0)
 #endif
 #ifndef RT_CAM_FRESH_SEG
 #define RT_CAM_FRESH_SEG 0 // also at every path segment (background, depth budget)
@@ -428,8 +431,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     // the epilogue's launch fields, camera width / scale and output pointer
     // read afresh (RT_EPI_FRESH): once per unit, outside the path loop, so the
     // one-unit instances need not hold them in SGPRs across every path trip
-    const DCamera Ce = camera_fields<kCamFresh || RT_EPI_FRESH>(C);
-    const DLaunch PE = launch_fields<(PC && RT_KARG_FRESH) || RT_EPI_FRESH>(P);
+    constexpr bool kEpiFresh = RT_EPI_FRESH_F(F);
+    const DCamera Ce = camera_fields<kCamFresh || kEpiFresh>(C);
+    const DLaunch PE = launch_fields<(PC && RT_KARG_FRESH) || kEpiFresh>(P);
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
     // whole units: the frame (pixels outside the image are not written) or
     // the compact tile layout; split units: their chunk's partial sums
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
         sy = Ce.scale * sy;
         sz = Ce.scale * sz;
       }
-      double *const ob = out_arg<(PC && RT_KARG_FRESH) || RT_EPI_FRESH>(out);
+      double *const ob = out_arg<(PC && RT_KARG_FRESH) || kEpiFresh>(out);
       const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
       double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
                   : PE.compact ? ob + 3 * ((size_t)unit * 64 + lane)
