@@ -305,6 +305,8 @@ typedef struct rt_scene_info {
                                    item and sphere in LDS (whole tree staged and room left) */
   int32_t persistent_block_waves; /* waves per block of the persistent instance: 16 (one block
                                      per CU) or 4 (traversal stacks too deep for 16); 0: none */
+  int32_t lds_perlin; /* 1: the scene's Perlin table (one noise texture source) is staged in
+                         LDS by every block of the noise instances; 0: read from HBM */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

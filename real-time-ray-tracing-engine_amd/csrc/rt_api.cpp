@@ -28,6 +28,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
 extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
 extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes);
 extern "C" int rtk_lds_prims_enabled(void);
+extern "C" int rtk_lds_perlin_enabled(void);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
 extern "C" size_t rtk_sah_temp_bytes(int n);
 extern "C" hipError_t rtk_build_sah(const double *boxes, const DItem *items_in, int n,
@@ -488,6 +489,13 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       d.lds_spheres_pc = (int32_t)H.spheres.size();
     }
   }
+  // the one Perlin table of a noise scene in LDS (RTX_LDS_PERLIN=0: from HBM,
+  // A/B runs and the bit-identity test); several tables stay in HBM
+  {
+    const char *pe = std::getenv("RTX_LDS_PERLIN");
+    d.lds_perlin = (d.features & RT_FEAT_NOISE) && H.perlin.size() == 1 && rtk_lds_perlin_enabled() &&
+                   !(pe && pe[0] == '0');
+  }
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
   s->unit_ctr = (int32_t *)(s->block + parts[iUc].off);
 
@@ -515,6 +523,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.lds_nodes_persistent = d.n_lds_nodes_pc;
   in.lds_prims_persistent = d.lds_items_pc > 0;
   in.persistent_block_waves = d.pc_waves;
+  in.lds_perlin = d.lds_perlin;
   *out = s;
   return RT_OK;
 }

@@ -332,6 +332,16 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
     __syncthreads();
   }
+#if RT_LDS_PERLIN
+  if constexpr ((F & F_NOISE) != 0) { // the Perlin table (tex_value), once per block
+    if (S.lds_perlin) {
+      const int4 *src = reinterpret_cast<const int4 *>(S.perlin);
+      RT_LDS int4 *dst = (RT_LDS int4 *)perlin_lds();
+      for (int k = threadIdx.x; k < (int)(sizeof(DPerlin) / 16); k += blockDim.x) dst[k] = src[k];
+      __syncthreads();
+    }
+  }
+#endif
   // work unit = (local tile, stratum chunk).  Persistent launches (P.unit_ctr
   // set, grid = the resident waves): a wave's first unit is its static slot,
   // the next ones come from the agent-scope counter (initialised by the host to
@@ -626,6 +636,7 @@ extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, i
   return hipSuccess;
 }
 extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
+extern "C" int rtk_lds_perlin_enabled(void) { return RT_LDS_PERLIN; }
 
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,

@@ -174,6 +174,8 @@ struct DScene {      // kernel argument (by value)
   int32_t lds_spheres_pc; // instance stages after its nodes (0: primitives stay in HBM)
   int32_t pc_waves;       // waves per block of the persistent instance: RT_PC_WAVES (one
                           // block per CU) or 4 (deep trees); 0: no persistent launches
+  int32_t lds_perlin;     // 1: the scene's one Perlin table is staged in LDS by the noise
+                          // instances' blocks (perlin_lds); 0: read from HBM
 };
 
 // Scene features (kernel specialisation keys)

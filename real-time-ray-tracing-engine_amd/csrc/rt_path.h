@@ -311,18 +311,19 @@ RT_HD RT_FI double sin_n(double x) {
 #ifndef RT_PERLIN_LERP
 #define RT_PERLIN_LERP 1 // C4 +6.6 % (4-wave blocks, r03g) and +5.3 % (one-wave blocks: r03h 3,207 vs r03j 3,047)
 #endif
-RT_HD double perlin_noise(const DPerlin &P, V3 p) {
+template <class PP> // const DPerlin *, or the LDS copy's pointer (RT_LDS)
+RT_HD double perlin_noise(PP P, V3 p) {
   double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
   double u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int xi = (int)fx, yi = (int)fy, zi = (int)fz;
   double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
 #if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP
-  const int px0 = P.px[xi & 255], px1 = P.px[(xi + 1) & 255];
-  const int py0 = P.py[yi & 255], py1 = P.py[(yi + 1) & 255];
-  const int pz0 = P.pz[zi & 255], pz1 = P.pz[(zi + 1) & 255];
+  const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
+  const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
+  const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
   const double u1 = u - 1, v1 = v - 1, w1 = w - 1;
   auto dotc = [&](int h, double di, double dj, double dk) {
-    const double *g = P.rv[h];
+    const auto *g = P->rv[h];
     return fma(g[0], di, fma(g[1], dj, g[2] * dk));
   };
   auto lerp = [](double a, double b, double t) { return fma(t, b - a, a); };
@@ -336,13 +337,13 @@ RT_HD double perlin_noise(const DPerlin &P, V3 p) {
 #endif
   double acc = 0.0;
   for (int i = 0; i < 2; i++) {
-    int pxi = P.px[(xi + i) & 255];
+    int pxi = P->px[(xi + i) & 255];
     double fi = i ? uu : 1 - uu, di = i ? u - 1 : u;
     for (int j = 0; j < 2; j++) {
-      int pyj = P.py[(yi + j) & 255];
+      int pyj = P->py[(yi + j) & 255];
       double fj = j ? vv : 1 - vv, dj = j ? v - 1 : v;
       for (int k = 0; k < 2; k++) {
-        const double *g = P.rv[pxi ^ pyj ^ P.pz[(zi + k) & 255]];
+        const auto *g = P->rv[pxi ^ pyj ^ P->pz[(zi + k) & 255]];
         double fk = k ? ww : 1 - ww, dk = k ? w - 1 : w;
         acc += fi * fj * fk * (g[0] * di + g[1] * dj + g[2] * dk);
       }
@@ -350,6 +351,24 @@ RT_HD double perlin_noise(const DPerlin &P, V3 p) {
   }
   return acc;
 }
+
+#ifndef RT_LDS_PERLIN
+#define RT_LDS_PERLIN 1
+#endif
+#if defined(__HIP__)
+// The block's LDS copy of the scene's Perlin table (9 KB; allocated in the
+// noise instances only -- the ones that call this).
+__device__ __forceinline__ const RT_LDS DPerlin *perlin_lds() {
+  __shared__ DPerlin table;
+  return (const RT_LDS DPerlin *)&table;
+}
+#endif
+
+// The octave loop stays rolled: unrolled, the scheduler overlaps the octaves'
+// independent LDS reads and the noise instances spill ~100 VGPRs.
+#ifndef RT_TURB_NOUNROLL
+#define RT_TURB_NOUNROLL 1
+#endif
 
 template <unsigned F>
 RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
@@ -364,14 +383,27 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
     }
     if constexpr ((F & F_NOISE) != 0) {
       // NoiseTexture.cpp:31-34: 0.5 * (1 + sin(scale*z + 10*turb(p, 7)))
-      const DPerlin &P = S.perlin[T.perlin];
-      double acc = 0.0, wgt = 1.0;
-      V3 q = p;
-      for (int i = 0; i < 7; i++) {
-        acc += wgt * perlin_noise(P, q);
-        wgt *= 0.5;
-        q = v3(q.x * 2, q.y * 2, q.z * 2);
-      }
+      auto turb = [&](auto P) { // PerlinNoise::turb(p, 7)
+        double acc = 0.0, wgt = 1.0;
+        V3 q = p;
+#if RT_TURB_NOUNROLL
+#pragma unroll 1
+#endif
+        for (int i = 0; i < 7; i++) {
+          acc += wgt * perlin_noise(P, q);
+          wgt *= 0.5;
+          q = v3(q.x * 2, q.y * 2, q.z * 2);
+        }
+        return acc;
+      };
+#if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_PERLIN
+      // the scene's one Perlin table staged in LDS by the block (S.lds_perlin):
+      // 7 octaves x (6 permutation + 8 gradient reads), two dependent rounds
+      // each, at LDS rather than L1/L2 latency
+      const double acc = S.lds_perlin ? turb(perlin_lds()) : turb(&S.perlin[T.perlin]);
+#else
+      const double acc = turb(&S.perlin[T.perlin]);
+#endif
 #if RT_SIN_N
       double f = 1 + sin_n(T.scale * p.z + 10 * fabs(acc));
 #else

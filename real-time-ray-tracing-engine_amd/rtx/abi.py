@@ -62,11 +62,7 @@ class SceneDesc(C.Structure):
                 ("n_objects", C.c_int32), ("objects", C.POINTER(ObjectDesc)),
                 ("children", C.POINTER(C.c_int32)), ("n_children", C.c_int32),
                 ("world", C.c_int32), ("lights", C.c_int32), ("use_bvh", C.c_int32),
-                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32),
-                ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
-                ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
-                ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32),
-                ("persistent_block_waves", C.c_int32)]
+                ("bvh_builder", C.c_int32), ("bvh_arity", C.c_int32)]
 
 
 RT_BVH_AUTO, RT_BVH_HOST, RT_BVH_DEVICE, RT_BVH_DEVICE_SAH = 0, 1, 2, 3
@@ -122,7 +118,7 @@ class SceneInfo(C.Structure):
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
                 ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
                 ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32),
-                ("persistent_block_waves", C.c_int32)]
+                ("persistent_block_waves", C.c_int32), ("lds_perlin", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

@@ -165,3 +165,35 @@ def test_deep_object_nesting_is_rejected_not_overflowing():
     h = C.c_void_p()
     assert L.rt_scene_create(C.byref(d), 0, C.byref(h)) == abi.RT_ERR_UNSUPPORTED
     assert b"nested deeper" in L.rt_last_error()
+
+
+def test_ctypes_mirror_matches_header_compiled_layout(tmp_path):
+    """Every ctypes Structure in rtx/abi.py has the size and the field offsets
+    gcc gives the header's struct of the same name (fields named alike)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    pairs = [(abi.Vec3, "rt_vec3"), (abi.TextureDesc, "rt_texture_desc"),
+             (abi.PerlinDesc, "rt_perlin_desc"), (abi.MaterialDesc, "rt_material_desc"),
+             (abi.ObjectDesc, "rt_object_desc"), (abi.SceneDesc, "rt_scene_desc"),
+             (abi.CameraDesc, "rt_camera_desc"), (abi.Frame, "rt_frame"),
+             (abi.RenderParams, "rt_render_params"), (abi.PathStats, "rt_path_stats"),
+             (abi.SceneInfo, "rt_scene_info")]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt_api.h"', "int main(void) {"]
+    want = []
+    for py, cn in pairs:
+        lines.append('printf("%%zu\\n", sizeof(%s));' % cn)
+        want.append(C.sizeof(py))
+        for f in py._fields_:
+            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (cn, f[0]))
+            want.append(getattr(py, f[0]).offset)
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)],
+                   check=True, capture_output=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert got == want

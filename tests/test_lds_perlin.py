@@ -1,0 +1,51 @@
+"""The noise instances' LDS copy of the scene's Perlin table
+(rt_path.h perlin_lds, staged once per block in rt_kernel.hip): the fog
+scene's frame must be bit-identical with the table read from HBM
+(RTX_LDS_PERLIN=0 at scene creation: the same arithmetic, only the load
+source differs) and match the oracle.  Reference: NoiseTexture.cpp:29-30,
+PerlinNoise.hpp:43-60 (turb over 7 octaves)."""
+import os
+
+import numpy as np
+import pytest
+
+from rtx.render import Renderer, camera_frame
+from rtx.scene import load_scene
+import oracle_lib as O
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+SCENES = os.path.join(O.ROOT, "real-time-ray-tracing-engine_amd", "scenes")
+
+
+def _render(S, f, seed, rows, lds):
+    old = os.environ.get("RTX_LDS_PERLIN")
+    os.environ["RTX_LDS_PERLIN"] = "1" if lds else "0"
+    try:
+        with Renderer(S) as R:
+            return R.info(), R.render(f, seed=seed, rows=rows)
+    finally:
+        if old is None:
+            os.environ.pop("RTX_LDS_PERLIN", None)
+        else:
+            os.environ["RTX_LDS_PERLIN"] = old
+
+
+@pytest.mark.parametrize("width,spp", [(64, 64), (1920, 16)])
+def test_lds_perlin_bit_identical_to_hbm(width, spp):
+    S = load_scene(os.path.join(SCENES, "cornell_fog.json"))
+    cam = S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=8)
+    f = camera_frame(cam)
+    rows = (0, f.image_height) if width <= 64 else (500, 516)
+    info1, lds = _render(S, f, 9, rows, True)
+    info0, hbm = _render(S, f, 9, rows, False)
+    assert info1["lds_perlin"] == 1 and info0["lds_perlin"] == 0
+    assert np.array_equal(lds, hbm)
+    if width <= 64:
+        compare(lds, O.oracle_render(S, cam, O.MODE_COUNTER, 9, rows=rows, threads=16))
+
+
+def test_scenes_without_noise_stage_no_table():
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    with Renderer(S) as R:
+        assert R.info()["lds_perlin"] == 0
