@@ -49,6 +49,21 @@ using namespace rtp;
 #endif
 #define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? RT_REGEN_PLAIN : 1))
 #endif
+// Merged regeneration (kMR): refills happen inside the trip, after the trace,
+// sharing the shading event's Philox block (see the trip loop); RT_MERGE_MIN
+// idle lanes start new paths there.
+#ifndef RT_REGEN_MERGE
+#define RT_REGEN_MERGE 0 // measured: C2 -5 % (merged refills at 1 idle lane), -2 % with the camera read afresh; profiles/r03p_ab.log, r03q_ab.log
+#endif
+#ifndef RT_REGEN_MERGE_F
+#define RT_REGEN_MERGE_F(F) (RT_REGEN_MERGE != 0 && (F) == F_FLAT)
+#endif
+#ifndef RT_MERGE_CAM_FRESH
+#define RT_MERGE_CAM_FRESH 0 // the camera frame read afresh from the kernarg segment for the new rays
+#endif
+#ifndef RT_MERGE_MIN
+#define RT_MERGE_MIN 1
+#endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
 #endif
@@ -335,9 +350,21 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
 #if RT_LDS_PERLIN
   if constexpr ((F & F_NOISE) != 0) { // the Perlin table (tex_value), once per block
     if (S.lds_perlin) {
+#if RT_PERLIN_F32
+      // fp32 gradients (padded to 16 B), then the three permutation tables
+      RT_LDS DPerlinF *dst = (RT_LDS DPerlinF *)perlin_lds();
+      for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+        const double *g = S.perlin->rv[k];
+        *(RT_LDS float4 *)dst->rv[k] = make_float4((float)g[0], (float)g[1], (float)g[2], 0.0f);
+      }
+      const int4 *src = reinterpret_cast<const int4 *>(S.perlin->px);
+      RT_LDS int4 *dsti = (RT_LDS int4 *)dst->px;
+      for (int k = threadIdx.x; k < 3 * 256 / 4; k += blockDim.x) dsti[k] = src[k];
+#else
       const int4 *src = reinterpret_cast<const int4 *>(S.perlin);
       RT_LDS int4 *dst = (RT_LDS int4 *)perlin_lds();
       for (int k = threadIdx.x; k < (int)(sizeof(DPerlin) / 16); k += blockDim.x) dst[k] = src[k];
+#endif
       __syncthreads();
     }
   }
@@ -389,9 +416,14 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   ps.active = false;
   Key key{P.seed_lo, P.seed_hi, 0, 0};
 
+  constexpr bool kMR = RT_REGEN_MERGE_F(F);
+  static_assert(!kMR || !kCamFresh, "merged regeneration reads the camera argument");
   for (;;) {
     // ---- regeneration: idle lanes pull the next (pixel, stratum) items
+    // (merged instances: only when the whole wave is idle -- the unit's start
+    // -- otherwise in the merged phase below)
     const uint64_t t_regen = STATS ? clk() : 0;
+    if (!kMR || __ballot(ps.active) == 0)
     for (;;) {
       unsigned long long idle = __ballot(!ps.active);
       if (idle == 0 || next_item >= n_items) break;
@@ -421,7 +453,73 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     if (STATS) cyc_regen += clk() - t_regen; // converged here (every lane)
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
-    if (ps.active) {
+    if constexpr (kMR) {
+      // ---- merged trip: trace; the misses end; then ONE Philox block per
+      // lane serves both the shading event of a lane that hit and the camera
+      // jitter of an idle lane taking a new (pixel, stratum) item -- the lanes
+      // that missed are exactly the ones idle in the shading code, so they
+      // draw their next camera ray there instead of in a refill pass of its own
+      Hit h;
+      const uint64_t t0 = STATS ? clk() : 0;
+      if (ps.active) {
+        if (STATS) n_segments++;
+        const bool hit = trace<STATS, F, PC && RT_LDS_PRIMS>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt,
+                                                            (RT_LDS LeafPool *)&leaf_pool[0], lp);
+        if (!hit) { // miss -> background (Camera.cpp:242-243); the path ends
+          ps.T = ps.T * ld3(C.bg);
+          atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
+          atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
+          atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
+          ps.active = false;
+        }
+      }
+      const uint64_t t1 = STATS ? clk() : 0;
+      if (STATS && wave_once()) cnt.ctrace += t1 - t0;
+      bool rg = false; // this lane starts a new path in this trip
+      int ri = 0, rj = 0;
+      {
+        const unsigned long long idle = __ballot(!ps.active);
+        if (idle != 0 && next_item < n_items && (__popcll(idle) >= RT_MERGE_MIN || ~idle == 0ull)) {
+          const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+          const int item = next_item + rank;
+          next_item += __popcll(idle);
+          if (!ps.active && item < n_items) {
+            const int slot = item & 63;
+            ri = x0 + (slot & 7);
+            rj = y0 + (slot >> 3);
+            if (ri < C.W && rj < P.row_end) {
+              rg = true;
+              ps.slot = slot;
+              ps.sample = s_first + (item >> 6);
+              key.pixel = (uint32_t)(rj * C.W + ri);
+              key.sample = (uint32_t)ps.sample;
+            }
+          }
+        }
+      }
+      // camera block: (pixel, stratum, kCamTag, slot 0); shading block:
+      // (pixel, stratum, bounce, kSlotShade = 0) -- the RNG contract's blocks
+      static_assert(kSlotShade == 0, "camera and shading blocks share slot 0");
+      double rn[4];
+      if (ps.active || rg) u01x4<F == F_FLAT>(key, rg ? kCamTag : ps.bounce, 0u, rn);
+      if (ps.active) {
+        const bool cont = shade<STATS, F, true>(S, C, ps, key, h, cnt, rn);
+        if (!cont) {
+          atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
+          atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
+          atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
+          ps.active = false;
+        }
+      }
+      if (rg) {
+        ps.ray = camera_ray_jt<F == F_FLAT>(camera_fields<RT_MERGE_CAM_FRESH != 0>(C), key, ri, rj, ps.sample, rn);
+        ps.T = v3(1.0, 1.0, 1.0);
+        ps.bounce = 0;
+        ps.active = C.max_depth > 0;
+        if (STATS) n_samples++;
+      }
+      if (STATS && wave_once()) cnt.cshade += clk() - t1;
+    } else if (ps.active) {
       if (STATS) n_segments++;
       bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
           scene_fields<RT_SCENE_FRESH && kCamFresh>(S), camera_fields<RT_CAM_FRESH_SEG && kCamFresh>(C), ps,

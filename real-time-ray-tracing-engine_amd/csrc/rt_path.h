@@ -352,15 +352,81 @@ RT_HD double perlin_noise(PP P, V3 p) {
   return acc;
 }
 
+// RT_PERLIN_F32 (device build): each octave's lattice cell and offsets are
+// found in fp64 exactly as above (floor, p - floor(p)), then the 8 corner dot
+// products and the Hermite blend run in fp32 on fp32 gradients, and the 7
+// octaves are summed in fp32.  Perlin noise is continuous and only scales an
+// albedo (no branch reads it), so the rounding moves the texture value by
+// ~1e-7 and the image by far less than the 1e-4 parity bound; the fp32 VALU
+// rate is twice the fp64 one.  Gradients: the fp32 LDS copy (DPerlinF), or
+// the fp64 table converted on load (the same floats).
+#ifndef RT_PERLIN_F32
+#define RT_PERLIN_F32 0 // A/B variant (build_dbgPF) until measured
+#endif
+struct DPerlinF { // the LDS copy of a DPerlin for the fp32 noise (7 KB)
+  float rv[256][4]; // gradient xyz, pad (one 16-B read per corner)
+  int32_t px[256], py[256], pz[256];
+};
+static_assert(sizeof(DPerlin) == 256 * 24 + 3 * 1024, "DPerlin layout: rv, then px, py, pz");
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef RT_PERLIN_B96
+#define RT_PERLIN_B96 0 // gradients as 12-B reads (three VGPRs per corner in flight instead of four)
+#endif
+__device__ __forceinline__ void perlin_grad(const RT_LDS DPerlinF *P, int h, float &x, float &y, float &z) {
+#if RT_PERLIN_B96
+  const float3 g = *(const RT_LDS float3 *)P->rv[h];
+#else
+  const float4 g = *(const RT_LDS float4 *)P->rv[h];
+#endif
+  x = g.x;
+  y = g.y;
+  z = g.z;
+}
+__device__ __forceinline__ void perlin_grad(const DPerlin *P, int h, float &x, float &y, float &z) {
+  x = (float)P->rv[h][0];
+  y = (float)P->rv[h][1];
+  z = (float)P->rv[h][2];
+}
+template <class PP>
+__device__ __forceinline__ float perlin_noise_f32(PP P, V3 p) {
+  const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+  const float u = (float)(p.x - fx), v = (float)(p.y - fy), w = (float)(p.z - fz);
+  const int xi = (int)fx, yi = (int)fy, zi = (int)fz;
+  const float uu = u * u * (3.0f - 2.0f * u), vv = v * v * (3.0f - 2.0f * v), ww = w * w * (3.0f - 2.0f * w);
+  const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
+  const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
+  const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
+  const float u1 = u - 1.0f, v1 = v - 1.0f, w1 = w - 1.0f;
+  auto dotc = [&](int h, float di, float dj, float dk) {
+    float gx, gy, gz;
+    perlin_grad(P, h, gx, gy, gz);
+    return fmaf(gx, di, fmaf(gy, dj, gz * dk));
+  };
+  auto lerp = [](float a, float b, float t) { return fmaf(t, b - a, a); };
+  const float c000 = dotc(px0 ^ py0 ^ pz0, u, v, w), c100 = dotc(px1 ^ py0 ^ pz0, u1, v, w);
+  const float c010 = dotc(px0 ^ py1 ^ pz0, u, v1, w), c110 = dotc(px1 ^ py1 ^ pz0, u1, v1, w);
+  const float c001 = dotc(px0 ^ py0 ^ pz1, u, v, w1), c101 = dotc(px1 ^ py0 ^ pz1, u1, v, w1);
+  const float c011 = dotc(px0 ^ py1 ^ pz1, u, v1, w1), c111 = dotc(px1 ^ py1 ^ pz1, u1, v1, w1);
+  const float x00 = lerp(c000, c100, uu), x10 = lerp(c010, c110, uu);
+  const float x01 = lerp(c001, c101, uu), x11 = lerp(c011, c111, uu);
+  return lerp(lerp(x00, x10, vv), lerp(x01, x11, vv), ww);
+}
+#endif
+
 #ifndef RT_LDS_PERLIN
 #define RT_LDS_PERLIN 1
 #endif
+#if RT_PERLIN_F32
+using PerlinLds = DPerlinF;
+#else
+using PerlinLds = DPerlin;
+#endif
 #if defined(__HIP__)
-// The block's LDS copy of the scene's Perlin table (9 KB; allocated in the
-// noise instances only -- the ones that call this).
-__device__ __forceinline__ const RT_LDS DPerlin *perlin_lds() {
-  __shared__ DPerlin table;
-  return (const RT_LDS DPerlin *)&table;
+// The block's LDS copy of the scene's Perlin table (9 KB; 7 KB as DPerlinF;
+// allocated in the noise instances only -- the ones that call this).
+__device__ __forceinline__ const RT_LDS PerlinLds *perlin_lds() {
+  __shared__ PerlinLds table;
+  return (const RT_LDS PerlinLds *)&table;
 }
 #endif
 
@@ -384,6 +450,17 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
     if constexpr ((F & F_NOISE) != 0) {
       // NoiseTexture.cpp:31-34: 0.5 * (1 + sin(scale*z + 10*turb(p, 7)))
       auto turb = [&](auto P) { // PerlinNoise::turb(p, 7)
+#if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_F32
+        float acc = 0.0f, wgt = 1.0f;
+        V3 q = p;
+#pragma unroll 1
+        for (int i = 0; i < 7; i++) {
+          acc = fmaf(wgt, perlin_noise_f32(P, q), acc);
+          wgt *= 0.5f;
+          q = v3(q.x * 2, q.y * 2, q.z * 2);
+        }
+        return (double)acc;
+#else
         double acc = 0.0, wgt = 1.0;
         V3 q = p;
 #if RT_TURB_NOUNROLL
@@ -395,6 +472,7 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
           q = v3(q.x * 2, q.y * 2, q.z * 2);
         }
         return acc;
+#endif
       };
 #if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_PERLIN
       // the scene's one Perlin table staged in LDS by the block (S.lds_perlin):
@@ -1588,9 +1666,12 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 #ifndef RT_SHADE_MERGE_F
 #define RT_SHADE_MERGE_F(F) (RT_SHADE_MERGE != 0 && ((F) & ~F_BVH4) == 0)
 #endif
-template <bool STATS, unsigned F>
+// PRE: the shading event's Philox block was drawn by the caller (rnp: the
+// merged regeneration below draws it together with the camera blocks of the
+// lanes that start new paths).
+template <bool STATS, unsigned F, bool PRE = false>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
-                       const Hit &h, Counters &cnt) {
+                       const Hit &h, Counters &cnt, const double *rnp = nullptr) {
   const uint32_t b = ps.bounce;
   const DMat M = S.mats[h.mat];
   if (STATS) cnt.shade++;
@@ -1603,7 +1684,14 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     return false;
   }
   double rn[4]; // one block per shading event: (e0, e1, d0, d1)
-  u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
+  if constexpr (PRE) {
+    rn[0] = rnp[0];
+    rn[1] = rnp[1];
+    rn[2] = rnp[2];
+    rn[3] = rnp[3];
+  } else {
+    u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
+  }
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   constexpr bool kMerge = RT_SHADE_MERGE_F(F);
@@ -1796,12 +1884,12 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
   return cont;
 }
 
+// The camera ray of stratum k of pixel (i, j) from its slot-0 block jt
+// (jitter x, jitter y, time); the defocus block (slot 1) is drawn here.
 template <bool KB = false> // KB: philox10
-RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
+RT_HD RT_FI Ray camera_ray_jt(const DCamera &C, const Key &key, int i, int j, int k, const double jt[4]) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
   const double rs = C.rs; // 1.0 / sqrt_spp (host-formed)
-  double jt[4]; // slot 0: jitter x, jitter y, time
-  u01x4<KB>(key, kCamTag, 0, jt);
   const double ja = jt[0], jb = jt[1];
   double px = ((si + ja) * rs) - 0.5;
   double py = ((sj + jb) * rs) - 0.5;
@@ -1818,6 +1906,12 @@ RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k
     org = (org + (dx * ld3(C.disk_u))) + (dy * ld3(C.disk_v)); // Camera.cpp:226-230
   }
   return Ray{org, ps - org, jt[2]};
+}
+template <bool KB = false>
+RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
+  double jt[4]; // slot 0: jitter x, jitter y, time
+  u01x4<KB>(key, kCamTag, 0, jt);
+  return camera_ray_jt<KB>(C, key, i, j, k, jt);
 }
 
 

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Per-instance register use and spills from `make asm`'s resource remarks:
+python tools/regs.py [F ...]  (default: every render_tiles instance)."""
+import re
+import subprocess
+import sys
+
+t = open(__import__("os").environ.get("RES", "real-time-ray-tracing-engine_amd/build/asm/resource.txt")).read()
+cur, rows = None, {}
+for line in t.splitlines():
+    m = re.search(r"Function Name: (\S+)", line)
+    if m:
+        cur = m.group(1)
+        rows[cur] = {}
+        continue
+    m = re.search(r"remark: .*?(VGPRs|SGPRs|VGPRs Spill|SGPRs Spill|Occupancy \[waves/SIMD\]|ScratchSize \[bytes/lane\]): (\d+)", line)
+    if m and cur:
+        rows[cur][m.group(1)] = int(m.group(2))
+want = set(int(a) for a in sys.argv[1:])
+for k, v in rows.items():
+    m = re.search(r"render_tilesILb(\d)ELj(\d+)ELi(\d+)E", k)
+    if not m or (want and int(m.group(2)) not in want):
+        continue
+    print("STATS=%s F=%-2s PC=%-2s VGPR %3s SGPR %3s spillV %3s spillS %3s occ %s scratch %s" % (
+        m.group(1), m.group(2), m.group(3), v.get("VGPRs"), v.get("SGPRs"), v.get("VGPRs Spill"),
+        v.get("SGPRs Spill"), v.get("Occupancy [waves/SIMD]"), v.get("ScratchSize [bytes/lane]")))
