@@ -311,16 +311,13 @@ RT_HD RT_FI double sin_n(double x) {
 #ifndef RT_PERLIN_LERP
 #define RT_PERLIN_LERP 1 // C4 +6.6 % (4-wave blocks, r03g) and +5.3 % (one-wave blocks: r03h 3,207 vs r03j 3,047)
 #endif
-template <class PP> // const DPerlin *, or the LDS copy's pointer (RT_LDS)
-RT_HD double perlin_noise(PP P, V3 p) {
-  double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
-  double u = p.x - fx, v = p.y - fy, w = p.z - fz;
-  int xi = (int)fx, yi = (int)fy, zi = (int)fz;
-  double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
-#if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP
-  const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
-  const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
-  const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
+#if defined(__HIP_DEVICE_COMPILE__)
+// The device form's blend of one octave from its cell offsets (u, v, w), their
+// Hermite weights and the six permutation entries of the cell's corners.
+template <class PP>
+__device__ __forceinline__ double perlin_blend(PP P, double u, double v, double w, double uu, double vv,
+                                               double ww, int px0, int px1, int py0, int py1, int pz0,
+                                               int pz1) {
   const double u1 = u - 1, v1 = v - 1, w1 = w - 1;
   auto dotc = [&](int h, double di, double dj, double dk) {
     const auto *g = P->rv[h];
@@ -334,6 +331,19 @@ RT_HD double perlin_noise(PP P, V3 p) {
   const double x00 = lerp(c000, c100, uu), x10 = lerp(c010, c110, uu);
   const double x01 = lerp(c001, c101, uu), x11 = lerp(c011, c111, uu);
   return lerp(lerp(x00, x10, vv), lerp(x01, x11, vv), ww);
+}
+#endif
+template <class PP> // const DPerlin *, or the LDS copy's pointer (RT_LDS)
+RT_HD double perlin_noise(PP P, V3 p) {
+  double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+  double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  int xi = (int)fx, yi = (int)fy, zi = (int)fz;
+  double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+#if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP
+  const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
+  const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
+  const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
+  return perlin_blend(P, u, v, w, uu, vv, ww, px0, px1, py0, py1, pz0, pz1);
 #endif
   double acc = 0.0;
   for (int i = 0; i < 2; i++) {
@@ -361,7 +371,7 @@ RT_HD double perlin_noise(PP P, V3 p) {
 // rate is twice the fp64 one.  Gradients: the fp32 LDS copy (DPerlinF), or
 // the fp64 table converted on load (the same floats).
 #ifndef RT_PERLIN_F32
-#define RT_PERLIN_F32 0 // A/B variant (build_dbgPF) until measured
+#define RT_PERLIN_F32 0 // measured C4 +0.25 %, within noise (profiles/r03r_ab.log): the reference arithmetic is kept
 #endif
 struct DPerlinF { // the LDS copy of a DPerlin for the fp32 noise (7 KB)
   float rv[256][4]; // gradient xyz, pad (one 16-B read per corner)
@@ -435,6 +445,9 @@ __device__ __forceinline__ const RT_LDS PerlinLds *perlin_lds() {
 #ifndef RT_TURB_NOUNROLL
 #define RT_TURB_NOUNROLL 1
 #endif
+#ifndef RT_TURB_PIPE
+#define RT_TURB_PIPE 0 // measured C4 -1.5 % (7 more spilled VGPRs in the noise instance; profiles/r03s_ab.log)
+#endif
 
 template <unsigned F>
 RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
@@ -460,6 +473,35 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
           q = v3(q.x * 2, q.y * 2, q.z * 2);
         }
         return (double)acc;
+#elif defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP && RT_TURB_PIPE
+        // the next octave's cell and permutation entries are read while this
+        // octave blends (one dependent LDS round per octave instead of two);
+        // the same operations on the same values as perlin_noise
+        double acc = 0.0, wgt = 1.0;
+        V3 q = p;
+        double fx = floor(q.x), fy = floor(q.y), fz = floor(q.z);
+        int xi = (int)fx, yi = (int)fy, zi = (int)fz;
+        int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
+        int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
+        int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
+#pragma unroll 1
+        for (int i = 0; i < 7; i++) {
+          const V3 q2 = v3(q.x * 2, q.y * 2, q.z * 2);
+          const double gx = floor(q2.x), gy = floor(q2.y), gz = floor(q2.z);
+          const int xj = (int)gx, yj = (int)gy, zj = (int)gz;
+          // (octave 7's reads are never used; the table has no bounds to pass)
+          const int nx0 = P->px[xj & 255], nx1 = P->px[(xj + 1) & 255];
+          const int ny0 = P->py[yj & 255], ny1 = P->py[(yj + 1) & 255];
+          const int nz0 = P->pz[zj & 255], nz1 = P->pz[(zj + 1) & 255];
+          const double u = q.x - fx, v = q.y - fy, w = q.z - fz;
+          const double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+          acc += wgt * perlin_blend(P, u, v, w, uu, vv, ww, px0, px1, py0, py1, pz0, pz1);
+          wgt *= 0.5;
+          q = q2;
+          fx = gx, fy = gy, fz = gz;
+          px0 = nx0, px1 = nx1, py0 = ny0, py1 = ny1, pz0 = nz0, pz1 = nz1;
+        }
+        return acc;
 #else
         double acc = 0.0, wgt = 1.0;
         V3 q = p;
