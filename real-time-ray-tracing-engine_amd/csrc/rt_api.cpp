@@ -26,7 +26,8 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
 extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes);
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes,
+                                      int *blocks_per_cu);
 extern "C" int rtk_lds_prims_enabled(void);
 extern "C" int rtk_lds_perlin_enabled(void);
 extern "C" size_t rtk_lbvh_temp_bytes(int n);
@@ -62,6 +63,7 @@ struct rt_scene {
   double *scratch = nullptr; // chunk partials of chunked frame launches
   size_t scratch_bytes = 0;
   int wave_slots = 0;        // resident waves of the render instance on this device
+  int pc_grid = 0;           // resident blocks of the persistent instance on this device
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
 };
 
@@ -469,8 +471,10 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     // persistent launches)
     int64_t pc_free = -1;
     int pcw = 0;
-    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pcw, &pc_free);
+    int pc_bpc = 0;
+    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pcw, &pc_free, &pc_bpc);
     d.pc_waves = pcw;
+    s->pc_grid = cus * pc_bpc;
     if (be != hipSuccess) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
@@ -577,7 +581,10 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   int target = 32;
   if (const char *t = std::getenv("RTX_CHUNK_TARGET")) target = std::atoi(t);
   if (target <= 0 || s->wave_slots <= 0) return sp;
-  const int64_t tiles = (int64_t)L.n_local_tiles, slots = s->wave_slots;
+  // wave slots of the instance that runs the launch (the persistent one's own
+  // residency for the feature sets that have one)
+  const int64_t tiles = (int64_t)L.n_local_tiles,
+                slots = s->pc_grid > 0 && s->ds.pc_waves > 0 ? (int64_t)s->pc_grid * s->ds.pc_waves : s->wave_slots;
   auto no_empty = [&](int64_t c) { // chunk count with no empty chunks
     c = std::max<int64_t>(1, std::min<int64_t>(c, L.sample_count));
     const int64_t cs = (L.sample_count + c - 1) / c;
@@ -640,7 +647,8 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   DLaunch Lp = L;
   if (persistent && s->wave_slots > 0) {
     Lp.unit_ctr = s->unit_ctr;
-    Lp.grid_cap = std::max(1, s->wave_slots / std::max(1, s->ds.pc_waves)); // resident persistent blocks
+    Lp.grid_cap = s->pc_grid > 0 ? s->pc_grid // resident persistent blocks
+                                 : std::max(1, s->wave_slots / std::max(1, s->ds.pc_waves));
     // RT_GRID_CAP: fewer resident blocks (tests: many units per wave)
     if (const char *g = getenv("RT_GRID_CAP"))
       if (atoi(g) > 0) Lp.grid_cap = atoi(g);

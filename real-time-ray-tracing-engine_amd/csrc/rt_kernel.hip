@@ -124,6 +124,14 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 #define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0 || (RT_PERSIST_FLAT && (F) == F_FLAT))
 #endif
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
+// occupancy target of the persistent instances (default: their feature set's)
+#ifndef RT_WAVES_PC
+#ifdef RT_WAVES_PC_N
+#define RT_WAVES_PC(F) RT_WAVES_PC_N
+#else
+#define RT_WAVES_PC(F) RT_WAVES_PER_EU(F)
+#endif
+#endif
 
 // The launch fields read afresh from the kernarg segment at each work unit
 // (FRESH, the persistent instances): the asm hides the segment pointer's
@@ -301,7 +309,7 @@ __device__ __forceinline__ double *out_arg(double *out) {
 // blocks of PCW waves (kPcWaves = one block per CU; kWaves when the traversal
 // stacks of 16 waves do not fit the CU's LDS, e.g. deep 4-wide trees)
 template <bool STATS, unsigned F, int PCW = 0>
-__global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(PCW ? RT_WAVES_PC(F) : RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   constexpr bool PC = PCW > 0;
   constexpr int BW = PC ? PCW : block_waves(F); // waves per block
@@ -710,9 +718,11 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
 // (one per SIMD at the occupancy target: a quarter of the CU's LDS each);
 // *pcw = 0 / *free_bytes = -1 when neither fits or the feature set has no
 // persistent instance.
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes) {
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes,
+                                      int *blocks_per_cu) {
   *free_bytes = -1;
   *pcw = 0;
+  *blocks_per_cu = 0;
   const unsigned f = (unsigned)(features & F_ALL);
   if (!RT_PERSIST_F(f)) return hipSuccess;
   const char *force = getenv("RTX_PC_WAVES"); // tests: the 4-wave form on any scene
@@ -723,10 +733,12 @@ extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, i
     if (e != hipSuccess) return e;
     const int regs = ((a.numRegs + 7) / 8) * 8;
     const int waves_per_simd = std::max(1, std::min(8, regs > 0 ? 512 / regs : 8));
-    const size_t per_block = kLdsPerCu / std::max(1, waves_per_simd * 4 / w);
+    const int bpc = std::max(1, waves_per_simd * 4 / w); // resident blocks per CU
+    const size_t per_block = kLdsPerCu / bpc;
     const size_t fixed = a.sharedSizeBytes + lds_bytes_pc(features, w, stack_depth, 0);
     if (fixed <= per_block) {
       *pcw = w;
+      *blocks_per_cu = bpc;
       *free_bytes = (int64_t)(per_block - fixed);
       return hipSuccess;
     }
