@@ -211,20 +211,76 @@ RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]
 #ifndef RT_SINCOS_2PI
 #define RT_SINCOS_2PI 1
 #endif
+// Polynomial constants at their use (RT_KCONST, device): fma(a, b, K) as ONE
+// v_fma_f64 whose addend K is put into an SGPR pair by two s_mov_b32 right
+// there (volatile, so not hoisted).  Written as plain fma, the compiler hoists
+// each fp64 coefficient out of the path loop into a VGPR pair (sincos: 10
+// pairs, 20 VGPRs live across the whole loop in every instance) and, because
+// it selects the tied v_fmac_f64 form, copies the constant into the
+// accumulator before every step (v_mov_b64 + v_fmac_f64).  Same correctly
+// rounded fma, same bits.
+#ifndef RT_KCONST
+#define RT_KCONST 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
+template <uint64_t K>
+__device__ __forceinline__ double kconst_s() { // K's double in an SGPR pair, materialised here
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3" : "=s"(lo), "=s"(hi) : "i"((uint32_t)K), "i"((uint32_t)(K >> 32)));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <uint64_t K>
+__device__ __forceinline__ double fma_k(double a, double b) { // fma(a, b, K)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(kconst_s<K>()));
+  return r;
+}
+template <uint64_t B, uint64_t K>
+__device__ __forceinline__ double fma_kk(double a) { // fma(a, B, K): B from SGPRs, K copied to a VGPR
+  double r;
+  const double k = kconst_s<K>();
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(kconst_s<B>()), "v"(k));
+  return r;
+}
+#define RT_KB(x) __builtin_bit_cast(uint64_t, (double)(x))
+#define FMA_K(a, b, K) fma_k<RT_KB(K)>((a), (b))
+#define FMA_KK(a, B, K) fma_kk<RT_KB(B), RT_KB(K)>((a))
+#endif
+// Measured (profiles/r03v_ab.log): the plain BVH instances C3 +2.3 % (their
+// VGPR spills 20 -> 4), the flat instance C2 -1 %, the rich C4 -8 % (its SGPRs
+// are already spilled into VGPR lanes): used by the plain BVH instances only.
+#ifndef RT_KCONST_F
+#define RT_KCONST_F(F) (RT_KCONST != 0 && ((F) & ~F_BVH4) == 0)
+#endif
+// KC: the polynomial constants at their use (above)
+template <bool KC = false>
 RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
 #if RT_SINCOS_2PI
   const double t = 4.0 * u;
   const double q = floor(t + 0.5);
   const double x = (t - q) * 1.5707963267948966;
   const double z = x * x;
-  const double ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                                      2.75573137070700676789e-06), -1.98412698298579493134e-04),
-                        8.33333333332248946124e-03);
-  const double sn = fma(z * x, fma(z, ps, -1.66666666666666324348e-01), x);
-  const double pc =
-      z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                                   -2.75573143513906633035e-07), 2.48015872894767294178e-05),
-                     -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+  double ps, sn, pc;
+#if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
+  if constexpr (KC) {
+    ps = FMA_K(z, FMA_K(z, FMA_K(z, FMA_KK(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                 2.75573137070700676789e-06), -1.98412698298579493134e-04),
+               8.33333333332248946124e-03);
+    sn = fma(z * x, FMA_K(z, ps, -1.66666666666666324348e-01), x);
+    pc = z * FMA_K(z, FMA_K(z, FMA_K(z, FMA_K(z, FMA_KK(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                              -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                          -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+  } else
+#endif
+  {
+    ps = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                           2.75573137070700676789e-06), -1.98412698298579493134e-04),
+             8.33333333332248946124e-03);
+    sn = fma(z * x, fma(z, ps, -1.66666666666666324348e-01), x);
+    pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                         -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                        -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+  }
   const double hz = 0.5 * z, w = 1.0 - hz;
   const double cn = w + (((1.0 - w) - hz) + z * pc);
   const int qi = (int)q & 3;
@@ -1753,7 +1809,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     V3 x1 = diel ? r.d : h.n;
     if (metal) x1 = r.d - (2 * dot(r.d, h.n)) * h.n;
     u1 = unitv(x1);
-    if (!diel) sincos_2pi(lamb ? d0 : d1, sp1, cp1);
+    if (!diel) sincos_2pi<RT_KCONST_F(F)>(lamb ? d0 : d1, sp1, cp1);
     z1 = 1.0 - 2.0 * d0;
     if (diel) ct1 = fmin(dot(-u1, h.n), 1.0);
     s1 = sqrt_n(lamb ? d1 : (diel ? 1.0 - ct1 * ct1 : fmax(0.0, 1.0 - z1 * z1)));
@@ -1796,7 +1852,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     double z = 1.0 - 2.0 * d0;
     double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
     double sp, cp;
-    sincos_2pi(d1, sp, cp);
+    sincos_2pi<RT_KCONST_F(F)>(d1, sp, cp);
     V3 uv = v3(rr * cp, rr * sp, z);
     refl = unitv(refl) + (M.fuzz * uv);
     ps.T = ps.T * ld3(M.albedo);
@@ -1861,7 +1917,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
       }
     } else if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
       double sp, cp;
-      sincos_2pi(d0, sp, cp);
+      sincos_2pi<RT_KCONST_F(F)>(d0, sp, cp);
       double sr = sqrt_n(d1);
       V3 lc = v3(cp * sr, sp * sr, sqrt_n(1 - d1));
       gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
@@ -1869,7 +1925,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
       double z = 1.0 - 2.0 * d0;
       double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
       double sp, cp;
-      sincos_2pi(d1, sp, cp);
+      sincos_2pi<RT_KCONST_F(F)>(d1, sp, cp);
       gd = v3(rr * cp, rr * sp, z);
     }
   }
@@ -1928,7 +1984,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
 
 // The camera ray of stratum k of pixel (i, j) from its slot-0 block jt
 // (jitter x, jitter y, time); the defocus block (slot 1) is drawn here.
-template <bool KB = false> // KB: philox10
+template <bool KB = false, bool KC = false> // KB: philox10; KC: sincos_2pi
 RT_HD RT_FI Ray camera_ray_jt(const DCamera &C, const Key &key, int i, int j, int k, const double jt[4]) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
   const double rs = C.rs; // 1.0 / sqrt_spp (host-formed)
@@ -1943,17 +1999,17 @@ RT_HD RT_FI Ray camera_ray_jt(const DCamera &C, const Key &key, int i, int j, in
     const double a = dk[0], b = dk[1];
     double rr = sqrt_n(a);
     double s, c;
-    sincos_2pi(b, s, c);
+    sincos_2pi<KC>(b, s, c);
     double dx = rr * c, dy = rr * s;
     org = (org + (dx * ld3(C.disk_u))) + (dy * ld3(C.disk_v)); // Camera.cpp:226-230
   }
   return Ray{org, ps - org, jt[2]};
 }
-template <bool KB = false>
+template <bool KB = false, bool KC = false>
 RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
   double jt[4]; // slot 0: jitter x, jitter y, time
   u01x4<KB>(key, kCamTag, 0, jt);
-  return camera_ray_jt<KB>(C, key, i, j, k, jt);
+  return camera_ray_jt<KB, KC>(C, key, i, j, k, jt);
 }
 
 
