@@ -242,9 +242,19 @@ __device__ __forceinline__ double fma_kk(double a) { // fma(a, B, K): B from SGP
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(kconst_s<B>()), "v"(k));
   return r;
 }
+// The VGPR form (KC 2): K put into a VGPR pair by two v_mov_b32 right before
+// the fma (2 VALU, no SGPRs) -- for the rich instances, whose SGPRs are spent:
+// the constant register dies at the fma, so the tied v_fmac_f64 needs no copy.
+template <uint64_t K>
+__device__ __forceinline__ double kconst_v() {
+  uint32_t lo, hi;
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((uint32_t)K), "i"((uint32_t)(K >> 32)));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 #define RT_KB(x) __builtin_bit_cast(uint64_t, (double)(x))
 #define FMA_K(a, b, K) fma_k<RT_KB(K)>((a), (b))
 #define FMA_KK(a, B, K) fma_kk<RT_KB(B), RT_KB(K)>((a))
+#define KV(K) kconst_v<RT_KB(K)>()
 #endif
 // Measured (profiles/r03v_ab.log): the plain BVH instances C3 +2.3 % (their
 // VGPR spills 20 -> 4), the flat instance C2 -1 %, the rich C4 -8 % (its SGPRs
@@ -252,8 +262,14 @@ __device__ __forceinline__ double fma_kk(double a) { // fma(a, B, K): B from SGP
 #ifndef RT_KCONST_F
 #define RT_KCONST_F(F) (RT_KCONST != 0 && ((F) & ~F_BVH4) == 0)
 #endif
-// KC: the polynomial constants at their use (above)
-template <bool KC = false>
+// KC: the polynomial constants at their use (above): 1 in SGPRs, 2 in VGPRs
+#ifndef RT_KCONST_V
+#define RT_KCONST_V 0 // measured C4 -7.6 % (r03x_ab.log: 3,439 -> 3,177), though its 6 spilled VGPRs go to 0
+#endif
+#ifndef RT_KCONST_MODE
+#define RT_KCONST_MODE(F) (RT_KCONST_F(F) ? 1 : (RT_KCONST_V && ((F) & (F_MEDIA | F_LIGHTS | F_NOISE | F_XFORM)) ? 2 : 0))
+#endif
+template <int KC = 0>
 RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
 #if RT_SINCOS_2PI
   const double t = 4.0 * u;
@@ -262,7 +278,15 @@ RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
   const double z = x * x;
   double ps, sn, pc;
 #if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
-  if constexpr (KC) {
+  if constexpr (KC == 2) {
+    ps = fma(z, fma(z, fma(z, fma(z, KV(1.58969099521155010221e-10), KV(-2.50507602534068634195e-08)),
+                           KV(2.75573137070700676789e-06)), KV(-1.98412698298579493134e-04)),
+             KV(8.33333333332248946124e-03));
+    sn = fma(z * x, fma(z, ps, KV(-1.66666666666666324348e-01)), x);
+    pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, KV(-1.13596475577881948265e-11), KV(2.08757232129817482790e-09)),
+                                         KV(-2.75573143513906633035e-07)), KV(2.48015872894767294178e-05)),
+                        KV(-1.38888888888741095749e-03)), KV(4.16666666666666019037e-02));
+  } else if constexpr (KC == 1) {
     ps = FMA_K(z, FMA_K(z, FMA_K(z, FMA_KK(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
                                  2.75573137070700676789e-06), -1.98412698298579493134e-04),
                8.33333333332248946124e-03);
@@ -1690,6 +1714,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
   return sum;
 }
 
+template <int KC = 0>
 RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double r2) {
   int k = S.n_lights - 1;
   for (int i = 0; i < S.n_lights; ++i)
@@ -1711,7 +1736,7 @@ RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double 
     V3 uu = cross(w, vv);
     double z = 1 + r2 * (sqrt(1 - s.rr / d2) - 1);
     double sphi, cphi;
-    sincos_2pi(r1, sphi, cphi);
+    sincos_2pi<KC>(r1, sphi, cphi);
     double x = cphi * sqrt(1 - z * z);
     double y = sphi * sqrt(1 - z * z);
     d = ((x * uu) + (y * vv)) + (z * w);
@@ -1809,7 +1834,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     V3 x1 = diel ? r.d : h.n;
     if (metal) x1 = r.d - (2 * dot(r.d, h.n)) * h.n;
     u1 = unitv(x1);
-    if (!diel) sincos_2pi<RT_KCONST_F(F)>(lamb ? d0 : d1, sp1, cp1);
+    if (!diel) sincos_2pi<RT_KCONST_MODE(F)>(lamb ? d0 : d1, sp1, cp1);
     z1 = 1.0 - 2.0 * d0;
     if (diel) ct1 = fmin(dot(-u1, h.n), 1.0);
     s1 = sqrt_n(lamb ? d1 : (diel ? 1.0 - ct1 * ct1 : fmax(0.0, 1.0 - z1 * z1)));
@@ -1852,7 +1877,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     double z = 1.0 - 2.0 * d0;
     double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
     double sp, cp;
-    sincos_2pi<RT_KCONST_F(F)>(d1, sp, cp);
+    sincos_2pi<RT_KCONST_MODE(F)>(d1, sp, cp);
     V3 uv = v3(rr * cp, rr * sp, z);
     refl = unitv(refl) + (M.fuzz * uv);
     ps.T = ps.T * ld3(M.albedo);
@@ -1902,7 +1927,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   if constexpr ((F & F_LIGHTS) != 0) {
     if (e0 < 0.5 && have_lights) {
       const uint64_t t0 = STATS ? clk() : 0;
-      gd = lights_random(S, h.p, e1, d0, d1);
+      gd = lights_random<RT_KCONST_MODE(F)>(S, h.p, e1, d0, d1);
       from_light = true;
       if (STATS && wave_once()) cnt.clights += clk() - t0;
     }
@@ -1917,7 +1942,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
       }
     } else if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
       double sp, cp;
-      sincos_2pi<RT_KCONST_F(F)>(d0, sp, cp);
+      sincos_2pi<RT_KCONST_MODE(F)>(d0, sp, cp);
       double sr = sqrt_n(d1);
       V3 lc = v3(cp * sr, sp * sr, sqrt_n(1 - d1));
       gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
@@ -1925,7 +1950,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
       double z = 1.0 - 2.0 * d0;
       double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
       double sp, cp;
-      sincos_2pi<RT_KCONST_F(F)>(d1, sp, cp);
+      sincos_2pi<RT_KCONST_MODE(F)>(d1, sp, cp);
       gd = v3(rr * cp, rr * sp, z);
     }
   }
@@ -1984,7 +2009,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
 
 // The camera ray of stratum k of pixel (i, j) from its slot-0 block jt
 // (jitter x, jitter y, time); the defocus block (slot 1) is drawn here.
-template <bool KB = false, bool KC = false> // KB: philox10; KC: sincos_2pi
+template <bool KB = false, int KC = 0> // KB: philox10; KC: sincos_2pi
 RT_HD RT_FI Ray camera_ray_jt(const DCamera &C, const Key &key, int i, int j, int k, const double jt[4]) {
   int si = k % C.sqrt_spp, sj = k / C.sqrt_spp;
   const double rs = C.rs; // 1.0 / sqrt_spp (host-formed)
@@ -2005,7 +2030,7 @@ RT_HD RT_FI Ray camera_ray_jt(const DCamera &C, const Key &key, int i, int j, in
   }
   return Ray{org, ps - org, jt[2]};
 }
-template <bool KB = false, bool KC = false>
+template <bool KB = false, int KC = 0>
 RT_HD RT_FI Ray camera_ray(const DCamera &C, const Key &key, int i, int j, int k) {
   double jt[4]; // slot 0: jitter x, jitter y, time
   u01x4<KB>(key, kCamTag, 0, jt);
