@@ -7,7 +7,10 @@ on the GPU, against the full IEEE operations on the same device, bit for bit:
 * div_mk(x, b, 1/b) — the Markstein quotient from a shared reciprocal — on
   random operands, divisors with all-ones / power-of-two significands, and pi;
 * rcp_n(x) — the division lowering for 1/x without scaling and fixup — on
-  [2^-600, 2^600], all-ones significands, the unit range, and +inf.
+  [2^-600, 2^600], all-ones significands, the unit range, and +inf;
+* sincos_2pi with its polynomial constants materialised at their use (SGPR and
+  VGPR forms, RT_KCONST) against the form that holds them, and against the
+  host build (tests/native emulator) of the same function.
 
 tests/native/build/libdevcheck.so is test-only (tests/native/Makefile).
 """
@@ -88,3 +91,26 @@ def test_rcp_n_equals_reciprocal_on_device(dev):
     _, _, dq, dv = run(dev, x, np.zeros_like(x))
     ok = same_bits(dq, dv)
     assert ok.all(), (x[~ok][:4], dq[~ok][:4], dv[~ok][:4])
+
+
+def test_sincos_constant_forms_identical_on_device(dev):
+    dev.devcheck_sincos.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    dev.devcheck_sincos.restype = C.c_int
+    rng = np.random.default_rng(5)
+    u = np.concatenate([rng.integers(0, 2**32, 1_000_000).astype(np.float64) * 2.0**-32,
+                        np.arange(0, 4097, dtype=np.float64) / 4096.0 * (1 - 2.0**-32),
+                        np.array([0.0, 0.125, 0.25, 0.375, 0.5, 0.75, 1 - 2.0**-32])])
+    out = np.zeros(6 * len(u))
+    P = C.POINTER(C.c_double)
+    rc = dev.devcheck_sincos(u.ctypes.data_as(P), len(u), out.ctypes.data_as(P))
+    assert rc == 0, rc
+    s0, c0, s1, c1, s2, c2 = out.reshape(6, len(u))
+    for a, b in ((s1, s0), (c1, c0), (s2, s0), (c2, c0)):
+        ok = same_bits(a, b)
+        assert ok.all(), (u[~ok][:4], a[~ok][:4], b[~ok][:4])
+    emu = os.path.join(os.path.dirname(__file__), "native", "build", "libemu.so")
+    E = C.CDLL(emu)
+    E.emu_sincos_2pi.argtypes = [P, C.c_int, P, P]
+    hs, hc = np.zeros_like(u), np.zeros_like(u)
+    E.emu_sincos_2pi(u.ctypes.data_as(P), len(u), hs.ctypes.data_as(P), hc.ctypes.data_as(P))
+    assert same_bits(s0, hs).all() and same_bits(c0, hc).all()
