@@ -215,8 +215,12 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
 #ifndef RT_CAM_FRESH_SEG
 #define RT_CAM_FRESH_SEG 0 // also at every path segment (background, depth budget)
 #endif
+#ifndef RT_CAM_FRESH_PLAIN
+#define RT_CAM_FRESH_PLAIN 0 // the plain BVH instances too: spills 4 -> 0 VGPRs, C3 -0.3 % (profiles/r03aa_ab.log)
+#endif
 #ifndef RT_CAM_FRESH_F
-#define RT_CAM_FRESH_F(F) (RT_CAM_FRESH != 0 && ((F) & (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE)) != 0)
+#define RT_CAM_FRESH_F(F) ((RT_CAM_FRESH != 0 && ((F) & (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE)) != 0) || \
+                           (RT_CAM_FRESH_PLAIN != 0 && ((F) & ~F_BVH4) == 0))
 #endif
 template <bool FRESH>
 __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
