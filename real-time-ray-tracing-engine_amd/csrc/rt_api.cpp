@@ -601,7 +601,9 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   if (tiles > 4 * slots && tail > 0 && bounded) {
     const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
     sp.head_chunks = no_empty((L.sample_count + head_max - 1) / head_max);
-    sp.chunks = no_empty(8 * (int64_t)sp.head_chunks);
+    int split = 8; // tail chunks per head chunk (RTX_TAIL_SPLIT: A/B runs)
+    if (const char *t = std::getenv("RTX_TAIL_SPLIT")) split = std::max(1, std::atoi(t));
+    sp.chunks = no_empty(split * (int64_t)sp.head_chunks);
     sp.n_head = (int)(tiles - n_tail);
     if (sp.chunks <= 1) sp = SplitPlan{L.n_local_tiles, 1, 1};
     return sp;
