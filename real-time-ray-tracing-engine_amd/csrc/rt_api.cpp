@@ -566,7 +566,7 @@ int rt_scene_destroy(rt_scene *s) {
 //    the uniform split below (C3 -9 % with whole 256-strata tiles, -1.5 %
 //    with a 2-slot tail), and their partials would grow with the strata.
 //  * Otherwise every tile split, ~RTX_CHUNK_TARGET (default 32) units per
-//    wave slot (the round-1 rule).
+//    wave slot (the round-1 rule), the last tiles again in finer chunks.
 // RTX_CHUNK_TARGET=0: whole tiles only (tests).
 struct SplitPlan {
   int n_head, head_chunks, chunks; // head tiles, their chunks; the tail tiles' chunks
@@ -595,14 +595,14 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   int head_max = 64;
   if (const char *h = std::getenv("RTX_HEAD_STRATA")) head_max = std::max(1, std::atoi(h));
   const int64_t head_chunks = (L.sample_count + head_max - 1) / head_max;
+  int split = 8; // tail chunks per head chunk (RTX_TAIL_SPLIT: A/B runs)
+  if (const char *t = std::getenv("RTX_TAIL_SPLIT")) split = std::max(1, std::atoi(t));
   // partial records of a head/tail plan: bounded by 4 frames (a tail of
   // chunked tiles + head chunks); otherwise the uniform split
   const bool bounded = head_chunks == 1 || head_chunks * tiles <= 4 * tiles;
   if (tiles > 4 * slots && tail > 0 && bounded) {
     const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
     sp.head_chunks = no_empty((L.sample_count + head_max - 1) / head_max);
-    int split = 8; // tail chunks per head chunk (RTX_TAIL_SPLIT: A/B runs)
-    if (const char *t = std::getenv("RTX_TAIL_SPLIT")) split = std::max(1, std::atoi(t));
     sp.chunks = no_empty(split * (int64_t)sp.head_chunks);
     sp.n_head = (int)(tiles - n_tail);
     if (sp.chunks <= 1) sp = SplitPlan{L.n_local_tiles, 1, 1};
@@ -611,6 +611,19 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   const int64_t c = ((int64_t)target * slots + tiles - 1) / std::max<int64_t>(1, tiles);
   sp.chunks = no_empty(c);
   if (sp.chunks > 1) sp.n_head = 0;
+  // ... with the last `slots` x RTX_TAIL_TILES tiles in `split` times finer
+  // chunks when the frame has a tile per wave slot (C4, C5: the uniform
+  // units last 15 / 84 ms; RTX_UNIFORM_TAIL=1: on -- A/B runs until measured)
+  const char *ut = std::getenv("RTX_UNIFORM_TAIL");
+  if (ut && ut[0] == '1' && sp.chunks > 1 && tiles > slots && tail > 0) {
+    const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
+    const int tc = no_empty(split * (int64_t)sp.chunks);
+    if (tc > sp.chunks && n_tail < tiles) {
+      sp.head_chunks = sp.chunks;
+      sp.chunks = tc;
+      sp.n_head = (int)(tiles - n_tail);
+    }
+  }
   return sp;
 }
 
