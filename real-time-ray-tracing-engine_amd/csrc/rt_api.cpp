@@ -443,7 +443,14 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   // sibling of a node on the current root path; three per level for 4-wide
   // nodes); LDS prefix of the BFS-ordered nodes sized to what the instance's
   // occupancy leaves free
-  d.stack_depth = std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
+  // the walk pushes without an overflow check (rt_path.h trace): the depth the
+  // host sizes the stack from must be the tree's, never clamped below it
+  if (H.bvh_depth + 1 > RT_STACK_DEPTH) {
+    rt_scene_destroy(s);
+    return set_err(RT_ERR_UNSUPPORTED, "world BVH deeper than the traversal stack (" +
+                                           std::to_string(H.bvh_depth) + " levels)");
+  }
+  d.stack_depth = std::max(1, H.bvh_depth + 1);
   if (H.bvh_arity == 4) {
     d.features |= RT_FEAT_BVH4;
     d.n_nodes = (int32_t)H.nodes4.size();
@@ -458,13 +465,26 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
     }
-    if (!plan.stack_fits) { // the binary stack (<= RT_STACK_DEPTH entries) fits the smallest share
-      rt_scene_destroy(s);
-      return set_err(RT_ERR_UNSUPPORTED, "BVH traversal stacks exceed the per-block LDS budget");
-    }
     s->wave_slots = cus * 4 * plan.waves_per_simd;
     int budget = plan.n_nodes;
-    if (const char *ln = std::getenv("RTX_LDS_NODES")) budget = std::atoi(ln); // A/B experiments
+    if (!plan.stack_fits) {
+      // the traversal stacks and static LDS exceed the block's share at the
+      // occupancy target (a compiler or register change can move that share):
+      // stage no nodes and accept fewer resident blocks per CU, as long as
+      // one block still fits the 64 KB a block may use without opt-in
+      if (plan.fixed_bytes > 64 * 1024) {
+        rt_scene_destroy(s);
+        return set_err(RT_ERR_UNSUPPORTED, "BVH traversal stacks exceed the per-block LDS limit");
+      }
+      std::fprintf(stderr,
+                   "rtx: traversal stacks need %d B of LDS per block, above the %d B share at %d "
+                   "waves/SIMD: no BVH nodes staged, lower occupancy\n",
+                   (int)plan.fixed_bytes, (int)plan.block_budget, (int)plan.waves_per_simd);
+      budget = 0;
+      s->wave_slots = cus * plan.resident_waves_per_cu;
+    }
+    if (const char *ln = std::getenv("RTX_LDS_NODES")) // A/B experiments, within the plan
+      budget = std::min(std::atoi(ln), plan.n_nodes);
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
     // the persistent instance: its node prefix, then -- if the whole tree is
     // staged and room is left -- the world items and spheres (-1: no
@@ -482,7 +502,8 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     const int64_t node_b = (d.features & RT_FEAT_BVH4) ? (int64_t)sizeof(DNode4) : (int64_t)sizeof(DNode);
     d.n_lds_nodes_pc = pc_free < 0 ? -1 : (int32_t)std::min<int64_t>(pc_free / node_b, d.n_nodes);
     if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) // A/B experiments
-      if (d.n_lds_nodes_pc >= 0) d.n_lds_nodes_pc = std::min(std::atoi(ln), d.n_nodes);
+      if (d.n_lds_nodes_pc >= 0) // within what the plan leaves free
+        d.n_lds_nodes_pc = (int32_t)std::min<int64_t>({(int64_t)std::atoi(ln), d.n_nodes, pc_free / node_b});
     d.lds_items_pc = d.lds_spheres_pc = 0;
     const int64_t prim_b = (int64_t)(H.items.size() * sizeof(DItem) + H.spheres.size() * sizeof(DSphere));
     const char *lp_env = std::getenv("RTX_LDS_PRIMS"); // 0: A/B experiments

@@ -31,6 +31,8 @@
 
 #include <algorithm>
 #include <array>
+#include <mutex>
+#include <set>
 #include <utility>
 
 #include "rt_path.h"
@@ -48,21 +50,6 @@ using namespace rtp;
 #define RT_REGEN_PLAIN 16
 #endif
 #define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? RT_REGEN_PLAIN : 1))
-#endif
-// Merged regeneration (kMR): refills happen inside the trip, after the trace,
-// sharing the shading event's Philox block (see the trip loop); RT_MERGE_MIN
-// idle lanes start new paths there.
-#ifndef RT_REGEN_MERGE
-#define RT_REGEN_MERGE 0 // measured: C2 -5 % (merged refills at 1 idle lane), -2 % with the camera read afresh; profiles/r03p_ab.log, r03q_ab.log
-#endif
-#ifndef RT_REGEN_MERGE_F
-#define RT_REGEN_MERGE_F(F) (RT_REGEN_MERGE != 0 && (F) == F_FLAT)
-#endif
-#ifndef RT_MERGE_CAM_FRESH
-#define RT_MERGE_CAM_FRESH 0 // the camera frame read afresh from the kernarg segment for the new rays
-#endif
-#ifndef RT_MERGE_MIN
-#define RT_MERGE_MIN 1
 #endif
 #ifndef RT_BLOCK_WAVES
 #define RT_BLOCK_WAVES 4
@@ -108,21 +95,10 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 // whose waves pull work units from a counter): the plain BVH walks (C3 +3.4 %,
 // profiles/r02ab-af_*); the flat and the rich instances keep one unit per wave
 // -- the unit loop's extra live state cost them 2-20 %.
-// 0: lane 0 fetches the next unit when the current one ends (one atomic
-// round trip per unit of ~3 ms); 1: when it starts, one more register across
-// the unit (measured C3 -0.5 %, profiles/r02ae_unit_prefetch_ab.log)
-#ifndef RT_UNIT_PREFETCH
-#define RT_UNIT_PREFETCH 0
-#endif
 #ifndef RT_KARG_FRESH
 #define RT_KARG_FRESH 1
 #endif
-#ifndef RT_PERSIST_FLAT
-#define RT_PERSIST_FLAT 0
-#endif
-#ifndef RT_PERSIST_F
-#define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0 || (RT_PERSIST_FLAT && (F) == F_FLAT))
-#endif
+#define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0)
 #define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
 // occupancy target of the persistent instances (default: their feature set's)
 #ifndef RT_WAVES_PC
@@ -198,29 +174,15 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
     return P;
   }
 }
-// The camera read afresh from the kernarg segment where it is used (FRESH: the
-// rich instances, whose scene tables and path state leave no SGPRs for the
-// camera's 52 dwords across the path loop -- held there, they spilled into
-// VGPR lanes and every use cost a v_readlane).  Scalar loads through the
+// The epilogue's camera fields read afresh from the kernarg segment (FRESH:
+// once per work unit, outside the path loop, so the one-unit instances need
+// not hold them in SGPRs across every path trip).  Scalar loads through the
 // asm-hidden segment pointer: they stay at the use, the scalar cache serves them.
-#ifndef RT_CAM_FRESH
-#define RT_CAM_FRESH 0 // measured: C4 -17 % (every segment), -21 % (regeneration only); profiles/r03b_ab.log, r03c_ab.log
-#endif
 #ifndef RT_EPI_FRESH
 #define RT_EPI_FRESH 1 // non-flat instances only: the flat one measured -0.5 % kernel time with it (C2; C4 neutral); profiles/r03l_ab.log
 #endif
 #ifndef RT_EPI_FRESH_F
 #define RT_EPI_FRESH_F(F) (RT_EPI_FRESH != 0 && ((F) & F_FLAT) == 0)
-#endif
-#ifndef RT_CAM_FRESH_SEG
-#define RT_CAM_FRESH_SEG 0 // also at every path segment (background, depth budget)
-#endif
-#ifndef RT_CAM_FRESH_PLAIN
-#define RT_CAM_FRESH_PLAIN 0 // the plain BVH instances too: spills 4 -> 0 VGPRs, C3 -0.3 % (profiles/r03aa_ab.log)
-#endif
-#ifndef RT_CAM_FRESH_F
-#define RT_CAM_FRESH_F(F) ((RT_CAM_FRESH != 0 && ((F) & (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE)) != 0) || \
-                           (RT_CAM_FRESH_PLAIN != 0 && ((F) & ~F_BVH4) == 0))
 #endif
 template <bool FRESH>
 __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
@@ -251,48 +213,6 @@ __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
     return C;
   }
 }
-// The scene tables read afresh at each path segment (FRESH: A/B experiments).
-#ifndef RT_SCENE_FRESH
-#define RT_SCENE_FRESH 0
-#endif
-template <bool FRESH>
-__device__ __forceinline__ DScene scene_fields(const DScene &S) {
-  if constexpr (FRESH) {
-    auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ka));
-    const __attribute__((address_space(4))) DScene &K = ka->S;
-    DScene D;
-    D.nodes = K.nodes;
-    D.items = K.items;
-    D.mitems = K.mitems;
-    D.mbox = K.mbox;
-    D.bitems = K.bitems;
-    D.xforms = K.xforms;
-    D.spheres = K.spheres;
-    D.quads = K.quads;
-    D.media = K.media;
-    D.mats = K.mats;
-    D.texs = K.texs;
-    D.perlin = K.perlin;
-    D.lights = K.lights;
-    D.n_lights = K.n_lights;
-    D.n_nodes = K.n_nodes;
-    D.root_is_leaf = K.root_is_leaf;
-    D.n_root_items = K.n_root_items;
-    D.features = K.features;
-    D.n_mitems = K.n_mitems;
-    D.stack_depth = K.stack_depth;
-    D.n_lds_nodes = S.n_lds_nodes; // the instance's own prefix (PC: n_lds_nodes_pc)
-    D.static_spheres = K.static_spheres;
-    D.n_lds_nodes_pc = K.n_lds_nodes_pc;
-    D.lds_items_pc = K.lds_items_pc;
-    D.lds_spheres_pc = K.lds_spheres_pc;
-    D.pc_waves = K.pc_waves;
-    return D;
-  } else {
-    return S;
-  }
-}
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -317,7 +237,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
                                                     unsigned long long *stats) {
   constexpr bool PC = PCW > 0;
   constexpr int BW = PC ? PCW : block_waves(F); // waves per block
-  constexpr bool kCamFresh = RT_CAM_FRESH_F(F);
   // the persistent instance stages its own (larger) node prefix
   DScene S = S_;
   if constexpr (PC) S.n_lds_nodes = S_.n_lds_nodes_pc;
@@ -362,21 +281,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
 #if RT_LDS_PERLIN
   if constexpr ((F & F_NOISE) != 0) { // the Perlin table (tex_value), once per block
     if (S.lds_perlin) {
-#if RT_PERLIN_F32
-      // fp32 gradients (padded to 16 B), then the three permutation tables
-      RT_LDS DPerlinF *dst = (RT_LDS DPerlinF *)perlin_lds();
-      for (int k = threadIdx.x; k < 256; k += blockDim.x) {
-        const double *g = S.perlin->rv[k];
-        *(RT_LDS float4 *)dst->rv[k] = make_float4((float)g[0], (float)g[1], (float)g[2], 0.0f);
-      }
-      const int4 *src = reinterpret_cast<const int4 *>(S.perlin->px);
-      RT_LDS int4 *dsti = (RT_LDS int4 *)dst->px;
-      for (int k = threadIdx.x; k < 3 * 256 / 4; k += blockDim.x) dsti[k] = src[k];
-#else
       const int4 *src = reinterpret_cast<const int4 *>(S.perlin);
       RT_LDS int4 *dst = (RT_LDS int4 *)perlin_lds();
       for (int k = threadIdx.x; k < (int)(sizeof(DPerlin) / 16); k += blockDim.x) dst[k] = src[k];
-#endif
       __syncthreads();
     }
   }
@@ -395,11 +302,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   const uint64_t t_start = STATS ? clk() : 0;
   uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
   while (unit < n_units) { // wave-uniform
-#if RT_UNIT_PREFETCH
-  int next = n_units;
-  if (PC && P.unit_ctr != nullptr && lane == 0)
-    next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
   const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
   // (wave-uniform) head unit: tile unit / head_chunks; tail unit: a chunk of
   // the tail tile n_head + (unit - head units) / n_chunks
@@ -428,14 +330,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   ps.active = false;
   Key key{P.seed_lo, P.seed_hi, 0, 0};
 
-  constexpr bool kMR = RT_REGEN_MERGE_F(F);
-  static_assert(!kMR || !kCamFresh, "merged regeneration reads the camera argument");
   for (;;) {
     // ---- regeneration: idle lanes pull the next (pixel, stratum) items
-    // (merged instances: only when the whole wave is idle -- the unit's start
-    // -- otherwise in the merged phase below)
     const uint64_t t_regen = STATS ? clk() : 0;
-    if (!kMR || __ballot(ps.active) == 0)
     for (;;) {
       unsigned long long idle = __ballot(!ps.active);
       if (idle == 0 || next_item >= n_items) break;
@@ -446,7 +343,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       int item = next_item + rank;
       next_item += __popcll(idle);
       if (!ps.active && item < n_items) {
-        const DCamera Cr = camera_fields<kCamFresh>(C);
+        const DCamera &Cr = C;
         int slot = item & 63;
         int i = x0 + (slot & 7), j = y0 + (slot >> 3);
         if (i < Cr.W && j < P.row_end) {
@@ -465,77 +362,10 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     if (STATS) cyc_regen += clk() - t_regen; // converged here (every lane)
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
-    if constexpr (kMR) {
-      // ---- merged trip: trace; the misses end; then ONE Philox block per
-      // lane serves both the shading event of a lane that hit and the camera
-      // jitter of an idle lane taking a new (pixel, stratum) item -- the lanes
-      // that missed are exactly the ones idle in the shading code, so they
-      // draw their next camera ray there instead of in a refill pass of its own
-      Hit h;
-      const uint64_t t0 = STATS ? clk() : 0;
-      if (ps.active) {
-        if (STATS) n_segments++;
-        const bool hit = trace<STATS, F, PC && RT_LDS_PRIMS>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt,
-                                                            (RT_LDS LeafPool *)&leaf_pool[0], lp);
-        if (!hit) { // miss -> background (Camera.cpp:242-243); the path ends
-          ps.T = ps.T * ld3(C.bg);
-          atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
-          atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
-          atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
-          ps.active = false;
-        }
-      }
-      const uint64_t t1 = STATS ? clk() : 0;
-      if (STATS && wave_once()) cnt.ctrace += t1 - t0;
-      bool rg = false; // this lane starts a new path in this trip
-      int ri = 0, rj = 0;
-      {
-        const unsigned long long idle = __ballot(!ps.active);
-        if (idle != 0 && next_item < n_items && (__popcll(idle) >= RT_MERGE_MIN || ~idle == 0ull)) {
-          const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-          const int item = next_item + rank;
-          next_item += __popcll(idle);
-          if (!ps.active && item < n_items) {
-            const int slot = item & 63;
-            ri = x0 + (slot & 7);
-            rj = y0 + (slot >> 3);
-            if (ri < C.W && rj < P.row_end) {
-              rg = true;
-              ps.slot = slot;
-              ps.sample = s_first + (item >> 6);
-              key.pixel = (uint32_t)(rj * C.W + ri);
-              key.sample = (uint32_t)ps.sample;
-            }
-          }
-        }
-      }
-      // camera block: (pixel, stratum, kCamTag, slot 0); shading block:
-      // (pixel, stratum, bounce, kSlotShade = 0) -- the RNG contract's blocks
-      static_assert(kSlotShade == 0, "camera and shading blocks share slot 0");
-      double rn[4];
-      if (ps.active || rg) u01x4<F == F_FLAT>(key, rg ? kCamTag : ps.bounce, 0u, rn);
-      if (ps.active) {
-        const bool cont = shade<STATS, F, true>(S, C, ps, key, h, cnt, rn);
-        if (!cont) {
-          atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
-          atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
-          atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
-          ps.active = false;
-        }
-      }
-      if (rg) {
-        ps.ray = camera_ray_jt<F == F_FLAT, RT_KCONST_MODE(F)>(camera_fields<RT_MERGE_CAM_FRESH != 0>(C), key, ri, rj, ps.sample, rn);
-        ps.T = v3(1.0, 1.0, 1.0);
-        ps.bounce = 0;
-        ps.active = C.max_depth > 0;
-        if (STATS) n_samples++;
-      }
-      if (STATS && wave_once()) cnt.cshade += clk() - t1;
-    } else if (ps.active) {
+    if (ps.active) {
       if (STATS) n_segments++;
       bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
-          scene_fields<RT_SCENE_FRESH && kCamFresh>(S), camera_fields<RT_CAM_FRESH_SEG && kCamFresh>(C), ps,
-          key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp);
+          S, C, ps, key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp);
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
@@ -552,7 +382,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     // read afresh (RT_EPI_FRESH): once per unit, outside the path loop, so the
     // one-unit instances need not hold them in SGPRs across every path trip
     constexpr bool kEpiFresh = RT_EPI_FRESH_F(F);
-    const DCamera Ce = camera_fields<kCamFresh || kEpiFresh>(C);
+    const DCamera Ce = camera_fields<kEpiFresh>(C);
     const DLaunch PE = launch_fields<(PC && RT_KARG_FRESH) || kEpiFresh>(P);
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
     // whole units: the frame (pixels outside the image are not written) or
@@ -585,11 +415,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   }
   __builtin_amdgcn_wave_barrier();
   if constexpr (!PC) break;
-#if !RT_UNIT_PREFETCH
   int next = n_units;
   if (P.unit_ctr != nullptr && lane == 0)
     next = __hip_atomic_fetch_add(P.unit_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
   unit = P.unit_ctr != nullptr ? __builtin_amdgcn_readfirstlane(__shfl(next, 0)) : n_units;
   } // unit loop
   if (STATS) {
@@ -657,9 +485,6 @@ constexpr std::array<RenderFn, sizeof...(Fs)> instance_table(std::integer_sequen
 
 // the persistent instances (RT_PERSIST_F feature sets), blocks of pcw waves
 RenderFn persistent_instance(unsigned f, int pcw) {
-  if constexpr (RT_PERSIST_F(F_FLAT)) {
-    if (f == F_FLAT) return pcw == kPcWaves ? render_tiles<false, F_FLAT, kPcWaves> : render_tiles<false, F_FLAT, kWaves>;
-  }
   if (pcw == kPcWaves)
     return (f & F_BVH4) ? render_tiles<false, F_BVH4, kPcWaves> : render_tiles<false, 0u, kPcWaves>;
   return (f & F_BVH4) ? render_tiles<false, F_BVH4, kWaves> : render_tiles<false, 0u, kWaves>;
@@ -713,6 +538,9 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   plan->fixed_bytes = (int32_t)fixed;
   plan->stack_fits = fixed <= per_block;
   plan->n_nodes = per_block > fixed ? (int)((per_block - fixed) / node) : 0;
+  // stacks over the share: fewer blocks per CU (the host then stages no nodes)
+  const int lds_blocks = fixed > 0 ? (int)(lds_cu / fixed) : blocks_per_cu;
+  plan->resident_waves_per_cu = std::min(blocks_per_cu, std::max(1, lds_blocks)) * bw;
   return hipSuccess;
 }
 
@@ -752,6 +580,28 @@ extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, i
 extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
 extern "C" int rtk_lds_perlin_enabled(void) { return RT_LDS_PERLIN; }
 
+// Lets a persistent instance's blocks use more than 64 KB of dynamic LDS: set
+// once per device and function, to the most any scene's plan can ask for (the
+// CU's LDS less the static part), so scenes of different staged sizes used
+// from different host threads never lower it between another launch's check
+// and its dispatch.
+static hipError_t allow_cu_lds(RenderFn fn) {
+  static std::mutex mu;
+  static std::set<std::pair<int, const void *>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const void *f = reinterpret_cast<const void *>(fn);
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({dev, f})) return hipSuccess;
+  hipFuncAttributes a;
+  e = hipFuncGetAttributes(&a, f);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsPerCu - a.sharedSizeBytes));
+  if (e == hipSuccess) done.insert({dev, f});
+  return e;
+}
+
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream) {
@@ -773,9 +623,7 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
     launch_waves = S->pc_waves;
     lds = lds_bytes_pc(S->features, S->pc_waves, S->stack_depth, S->n_lds_nodes_pc) +
           (size_t)S->lds_items_pc * sizeof(DItem) + (size_t)S->lds_spheres_pc * sizeof(DSphere);
-    // beyond 64 KB of LDS per block (set on every launch: cheap, and per device)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = allow_cu_lds(fn);
     if (e != hipSuccess) return e;
     e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(Q.unit_ctr), blocks * S->pc_waves, 1, stream);
     if (e != hipSuccess) return e;

@@ -194,6 +194,7 @@ struct RtkLdsPlan {
   int32_t fixed_bytes;    // static LDS + traversal stacks per block
   int32_t stack_fits;     // fixed_bytes <= block_budget
   int32_t n_nodes;        // BVH nodes that fit in the rest (BFS prefix)
+  int32_t resident_waves_per_cu; // waves resident per CU with no nodes staged (LDS may limit it)
 };
 
 struct DCamera {     // the rt_frame values the kernel needs

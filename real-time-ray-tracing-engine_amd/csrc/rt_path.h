@@ -242,32 +242,20 @@ __device__ __forceinline__ double fma_kk(double a) { // fma(a, B, K): B from SGP
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(kconst_s<B>()), "v"(k));
   return r;
 }
-// The VGPR form (KC 2): K put into a VGPR pair by two v_mov_b32 right before
-// the fma (2 VALU, no SGPRs) -- for the rich instances, whose SGPRs are spent:
-// the constant register dies at the fma, so the tied v_fmac_f64 needs no copy.
-template <uint64_t K>
-__device__ __forceinline__ double kconst_v() {
-  uint32_t lo, hi;
-  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=v"(lo), "=v"(hi) : "i"((uint32_t)K), "i"((uint32_t)(K >> 32)));
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 #define RT_KB(x) __builtin_bit_cast(uint64_t, (double)(x))
 #define FMA_K(a, b, K) fma_k<RT_KB(K)>((a), (b))
 #define FMA_KK(a, B, K) fma_kk<RT_KB(B), RT_KB(K)>((a))
-#define KV(K) kconst_v<RT_KB(K)>()
 #endif
 // Measured (profiles/r03v_ab.log): the plain BVH instances C3 +2.3 % (their
 // VGPR spills 20 -> 4), the flat instance C2 -1 %, the rich C4 -8 % (its SGPRs
-// are already spilled into VGPR lanes): used by the plain BVH instances only.
+// are already spilled into VGPR lanes; constants put into VGPRs by v_mov at
+// their use instead: C4 -7.6 %, r03x_ab.log): used by the plain BVH instances only.
 #ifndef RT_KCONST_F
 #define RT_KCONST_F(F) (RT_KCONST != 0 && ((F) & ~F_BVH4) == 0)
 #endif
-// KC: the polynomial constants at their use (above): 1 in SGPRs, 2 in VGPRs
-#ifndef RT_KCONST_V
-#define RT_KCONST_V 0 // measured C4 -7.6 % (r03x_ab.log: 3,439 -> 3,177), though its 6 spilled VGPRs go to 0
-#endif
+// KC: 1 = the polynomial constants at their use in SGPRs (above), 0 = plain fma
 #ifndef RT_KCONST_MODE
-#define RT_KCONST_MODE(F) (RT_KCONST_F(F) ? 1 : (RT_KCONST_V && ((F) & (F_MEDIA | F_LIGHTS | F_NOISE | F_XFORM)) ? 2 : 0))
+#define RT_KCONST_MODE(F) (RT_KCONST_F(F) ? 1 : 0)
 #endif
 template <int KC = 0>
 RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
@@ -278,15 +266,7 @@ RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
   const double z = x * x;
   double ps, sn, pc;
 #if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
-  if constexpr (KC == 2) {
-    ps = fma(z, fma(z, fma(z, fma(z, KV(1.58969099521155010221e-10), KV(-2.50507602534068634195e-08)),
-                           KV(2.75573137070700676789e-06)), KV(-1.98412698298579493134e-04)),
-             KV(8.33333333332248946124e-03));
-    sn = fma(z * x, fma(z, ps, KV(-1.66666666666666324348e-01)), x);
-    pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, KV(-1.13596475577881948265e-11), KV(2.08757232129817482790e-09)),
-                                         KV(-2.75573143513906633035e-07)), KV(2.48015872894767294178e-05)),
-                        KV(-1.38888888888741095749e-03)), KV(4.16666666666666019037e-02));
-  } else if constexpr (KC == 1) {
+  if constexpr (KC == 1) {
     ps = FMA_K(z, FMA_K(z, FMA_K(z, FMA_KK(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
                                  2.75573137070700676789e-06), -1.98412698298579493134e-04),
                8.33333333332248946124e-03);
@@ -442,78 +422,12 @@ RT_HD double perlin_noise(PP P, V3 p) {
   return acc;
 }
 
-// RT_PERLIN_F32 (device build): each octave's lattice cell and offsets are
-// found in fp64 exactly as above (floor, p - floor(p)), then the 8 corner dot
-// products and the Hermite blend run in fp32 on fp32 gradients, and the 7
-// octaves are summed in fp32.  Perlin noise is continuous and only scales an
-// albedo (no branch reads it), so the rounding moves the texture value by
-// ~1e-7 and the image by far less than the 1e-4 parity bound; the fp32 VALU
-// rate is twice the fp64 one.  Gradients: the fp32 LDS copy (DPerlinF), or
-// the fp64 table converted on load (the same floats).
-#ifndef RT_PERLIN_F32
-#define RT_PERLIN_F32 0 // measured C4 +0.25 %, within noise (profiles/r03r_ab.log): the reference arithmetic is kept
-#endif
-struct DPerlinF { // the LDS copy of a DPerlin for the fp32 noise (7 KB)
-  float rv[256][4]; // gradient xyz, pad (one 16-B read per corner)
-  int32_t px[256], py[256], pz[256];
-};
-static_assert(sizeof(DPerlin) == 256 * 24 + 3 * 1024, "DPerlin layout: rv, then px, py, pz");
-#if defined(__HIP_DEVICE_COMPILE__)
-#ifndef RT_PERLIN_B96
-#define RT_PERLIN_B96 0 // gradients as 12-B reads (three VGPRs per corner in flight instead of four)
-#endif
-__device__ __forceinline__ void perlin_grad(const RT_LDS DPerlinF *P, int h, float &x, float &y, float &z) {
-#if RT_PERLIN_B96
-  const float3 g = *(const RT_LDS float3 *)P->rv[h];
-#else
-  const float4 g = *(const RT_LDS float4 *)P->rv[h];
-#endif
-  x = g.x;
-  y = g.y;
-  z = g.z;
-}
-__device__ __forceinline__ void perlin_grad(const DPerlin *P, int h, float &x, float &y, float &z) {
-  x = (float)P->rv[h][0];
-  y = (float)P->rv[h][1];
-  z = (float)P->rv[h][2];
-}
-template <class PP>
-__device__ __forceinline__ float perlin_noise_f32(PP P, V3 p) {
-  const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
-  const float u = (float)(p.x - fx), v = (float)(p.y - fy), w = (float)(p.z - fz);
-  const int xi = (int)fx, yi = (int)fy, zi = (int)fz;
-  const float uu = u * u * (3.0f - 2.0f * u), vv = v * v * (3.0f - 2.0f * v), ww = w * w * (3.0f - 2.0f * w);
-  const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
-  const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
-  const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
-  const float u1 = u - 1.0f, v1 = v - 1.0f, w1 = w - 1.0f;
-  auto dotc = [&](int h, float di, float dj, float dk) {
-    float gx, gy, gz;
-    perlin_grad(P, h, gx, gy, gz);
-    return fmaf(gx, di, fmaf(gy, dj, gz * dk));
-  };
-  auto lerp = [](float a, float b, float t) { return fmaf(t, b - a, a); };
-  const float c000 = dotc(px0 ^ py0 ^ pz0, u, v, w), c100 = dotc(px1 ^ py0 ^ pz0, u1, v, w);
-  const float c010 = dotc(px0 ^ py1 ^ pz0, u, v1, w), c110 = dotc(px1 ^ py1 ^ pz0, u1, v1, w);
-  const float c001 = dotc(px0 ^ py0 ^ pz1, u, v, w1), c101 = dotc(px1 ^ py0 ^ pz1, u1, v, w1);
-  const float c011 = dotc(px0 ^ py1 ^ pz1, u, v1, w1), c111 = dotc(px1 ^ py1 ^ pz1, u1, v1, w1);
-  const float x00 = lerp(c000, c100, uu), x10 = lerp(c010, c110, uu);
-  const float x01 = lerp(c001, c101, uu), x11 = lerp(c011, c111, uu);
-  return lerp(lerp(x00, x10, vv), lerp(x01, x11, vv), ww);
-}
-#endif
-
 #ifndef RT_LDS_PERLIN
 #define RT_LDS_PERLIN 1
 #endif
-#if RT_PERLIN_F32
-using PerlinLds = DPerlinF;
-#else
 using PerlinLds = DPerlin;
-#endif
 #if defined(__HIP__)
-// The block's LDS copy of the scene's Perlin table (9 KB; 7 KB as DPerlinF;
-// allocated in the noise instances only -- the ones that call this).
+// The block's LDS copy of the scene's Perlin table (9 KB; allocated in the noise instances only -- the ones that call this).
 __device__ __forceinline__ const RT_LDS PerlinLds *perlin_lds() {
   __shared__ PerlinLds table;
   return (const RT_LDS PerlinLds *)&table;
@@ -521,12 +435,13 @@ __device__ __forceinline__ const RT_LDS PerlinLds *perlin_lds() {
 #endif
 
 // The octave loop stays rolled: unrolled, the scheduler overlaps the octaves'
-// independent LDS reads and the noise instances spill ~100 VGPRs.
+// independent LDS reads and the noise instances spill ~100 VGPRs; software-
+// pipelined (the next octave's cell and permutation reads issued while this
+// octave blends) it measured C4 -1.5 % with 7 more spilled VGPRs
+// (profiles/r03s_ab.log).  fp32 octaves on an fp32 gradient copy: C4 +0.25 %,
+// within noise (r03r_ab.log), so the reference's fp64 arithmetic is kept.
 #ifndef RT_TURB_NOUNROLL
 #define RT_TURB_NOUNROLL 1
-#endif
-#ifndef RT_TURB_PIPE
-#define RT_TURB_PIPE 0 // measured C4 -1.5 % (7 more spilled VGPRs in the noise instance; profiles/r03s_ab.log)
 #endif
 
 template <unsigned F>
@@ -543,46 +458,6 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
     if constexpr ((F & F_NOISE) != 0) {
       // NoiseTexture.cpp:31-34: 0.5 * (1 + sin(scale*z + 10*turb(p, 7)))
       auto turb = [&](auto P) { // PerlinNoise::turb(p, 7)
-#if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_F32
-        float acc = 0.0f, wgt = 1.0f;
-        V3 q = p;
-#pragma unroll 1
-        for (int i = 0; i < 7; i++) {
-          acc = fmaf(wgt, perlin_noise_f32(P, q), acc);
-          wgt *= 0.5f;
-          q = v3(q.x * 2, q.y * 2, q.z * 2);
-        }
-        return (double)acc;
-#elif defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP && RT_TURB_PIPE
-        // the next octave's cell and permutation entries are read while this
-        // octave blends (one dependent LDS round per octave instead of two);
-        // the same operations on the same values as perlin_noise
-        double acc = 0.0, wgt = 1.0;
-        V3 q = p;
-        double fx = floor(q.x), fy = floor(q.y), fz = floor(q.z);
-        int xi = (int)fx, yi = (int)fy, zi = (int)fz;
-        int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
-        int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
-        int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
-#pragma unroll 1
-        for (int i = 0; i < 7; i++) {
-          const V3 q2 = v3(q.x * 2, q.y * 2, q.z * 2);
-          const double gx = floor(q2.x), gy = floor(q2.y), gz = floor(q2.z);
-          const int xj = (int)gx, yj = (int)gy, zj = (int)gz;
-          // (octave 7's reads are never used; the table has no bounds to pass)
-          const int nx0 = P->px[xj & 255], nx1 = P->px[(xj + 1) & 255];
-          const int ny0 = P->py[yj & 255], ny1 = P->py[(yj + 1) & 255];
-          const int nz0 = P->pz[zj & 255], nz1 = P->pz[(zj + 1) & 255];
-          const double u = q.x - fx, v = q.y - fy, w = q.z - fz;
-          const double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
-          acc += wgt * perlin_blend(P, u, v, w, uu, vv, ww, px0, px1, py0, py1, pz0, pz1);
-          wgt *= 0.5;
-          q = q2;
-          fx = gx, fy = gy, fz = gz;
-          px0 = nx0, px1 = nx1, py0 = ny0, py1 = ny1, pz0 = nz0, pz1 = nz1;
-        }
-        return acc;
-#else
         double acc = 0.0, wgt = 1.0;
         V3 q = p;
 #if RT_TURB_NOUNROLL
@@ -594,7 +469,6 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
           q = v3(q.x * 2, q.y * 2, q.z * 2);
         }
         return acc;
-#endif
       };
 #if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_PERLIN
       // the scene's one Perlin table staged in LDS by the block (S.lds_perlin):
@@ -704,9 +578,6 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
 #endif
 #ifndef RT_UNIFORM_LOADS
 #define RT_UNIFORM_LOADS 1 // scalar loads of wave-uniform scene records (ldu)
-#endif
-#ifndef RT_STACK_GUARD
-#define RT_STACK_GUARD 0 // traversal stack overflow check per push (trace)
 #endif
 // ... in the plain flat instance (C2 +2.7 %); the rich flat instances have no
 // SGPRs to spare for the records (C4 -1.6 %; profiles/r03d_ab.log)
@@ -1099,63 +970,15 @@ RT_HD RT_FI bool slab_hit(const RayF<true> &q, const float *lo, const float *hi,
 #endif
   return tl <= fmaf(th, kSlabGrow, q.slack);
 }
-// Both children of a binary node (slab_hit each).  RT_SLAB_PK (device): the
-// twelve plane FMAs as six packed fp32 FMAs (v_pk_fma_f32, full rate) on the
-// child-interleaved planes lo[axis][child] -- the same IEEE fma per element,
-// so the same entry distances and verdicts as twelve scalar fmaf.
-#ifndef RT_SLAB_PK
-#define RT_SLAB_PK 0 // measured C3 -2.1 %: 3 more spilled VGPRs outweigh 5 VALU per visit (profiles/r03k_ab.log)
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef float rt_f2 __attribute__((ext_vector_type(2)));
-#endif
+// Both children of a binary node (slab_hit each).  As six packed fp32 FMAs
+// (v_pk_fma_f32 on the child-interleaved planes) the visit is 5 VALU shorter
+// but the persistent instance spills 3 more VGPRs: C3 -2.1 % (r03k_ab.log).
 RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, float cl32, float &t0,
                            float &t1, bool &h0, bool &h1) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SLAB_PK
-  // the six per-ray constants in three register pairs (1/d_x, 1/d_y), (1/d_z,
-  // -p_x), (-p_y, -p_z), broadcast into both halves by op_sel -- the splat
-  // pairs the compiler builds otherwise take six more VGPRs across the walk
-  const rt_f2 k0 = {q.inv[0], q.inv[1]}, k1 = {q.inv[2], -q.p[0]}, k2 = {-q.p[1], -q.p[2]};
-  rt_f2 a[3], b[3];
-  const rt_f2 lx = {N.lo[0][0], N.lo[0][1]}, hx = {N.hi[0][0], N.hi[0][1]};
-  const rt_f2 ly = {N.lo[1][0], N.lo[1][1]}, hy = {N.hi[1][0], N.hi[1][1]};
-  const rt_f2 lz = {N.lo[2][0], N.lo[2][1]}, hz = {N.hi[2][0], N.hi[2][1]};
-  // x: k0.lo * plane + k1.hi;  y: k0.hi * plane + k2.lo;  z: k1.lo * plane + k2.hi
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(a[0]) : "v"(lx), "v"(k0), "v"(k1));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(b[0]) : "v"(hx), "v"(k0), "v"(k1));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(a[1]) : "v"(ly), "v"(k0), "v"(k2));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(b[1]) : "v"(hy), "v"(k0), "v"(k2));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(a[2]) : "v"(lz), "v"(k1), "v"(k2));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(b[2]) : "v"(hz), "v"(k1), "v"(k2));
-  // entry / exit distances in asm too: the packed FMAs' results come out of
-  // asm, which the compiler cannot prove canonical, so fminf / fmaxf would
-  // re-canonicalise each of them (one v_max per plane distance)
-  auto verdict = [&](float a0, float b0, float a1, float b1, float a2, float b2, float &tl) {
-    float n0, n1, n2, f0, f1, f2, th;
-    asm("v_min_f32 %[n0], %[a0], %[b0]\n\t"
-        "v_min_f32 %[n1], %[a1], %[b1]\n\t"
-        "v_min_f32 %[n2], %[a2], %[b2]\n\t"
-        "v_max_f32 %[n2], %[n2], %[tmin]\n\t"
-        "v_max3_f32 %[tl], %[n0], %[n1], %[n2]\n\t"
-        "v_max_f32 %[f0], %[a0], %[b0]\n\t"
-        "v_max_f32 %[f1], %[a1], %[b1]\n\t"
-        "v_max_f32 %[f2], %[a2], %[b2]\n\t"
-        "v_min3_f32 %[f2], %[f2], %[cl], %[f1]\n\t"
-        "v_min_f32 %[th], %[f0], %[f2]"
-        : [tl] "=&v"(tl), [th] "=&v"(th), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2),
-          [f0] "=&v"(f0), [f1] "=&v"(f1), [f2] "=&v"(f2)
-        : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1), [a2] "v"(a2), [b2] "v"(b2),
-          [tmin] "s"(tmin32), [cl] "v"(cl32));
-    return tl <= fmaf(th, kSlabGrow, q.slack);
-  };
-  h0 = verdict(a[0].x, b[0].x, a[1].x, b[1].x, a[2].x, b[2].x, t0);
-  h1 = verdict(a[0].y, b[0].y, a[1].y, b[1].y, a[2].y, b[2].y, t1);
-#else
   const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
   const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
   h0 = slab_hit(q, lo0, hi0, tmin32, cl32, t0);
   h1 = slab_hit(q, lo1, hi1, tmin32, cl32, t1);
-#endif
 }
 // f32_up(x) as a canonical float (the min/max operations take it as is
 // instead of re-canonicalising it at every box test)
@@ -1502,12 +1325,9 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     // sizes S.stack_depth to what the walk can push -- one entry per level of
     // the binary tree (a pushed entry is the sibling of a node on the current
     // root path), three per 4-wide level -- plus one, from the depth of the
-    // tree it built (RT_STACK_GUARD=1 restores the per-push check).
+    // tree it built (a per-push check measured C3 -2.3 %, profiles/r03h_ab.log).
     int *top = stk;
     auto push = [&](int e) {
-#if RT_STACK_GUARD
-      if (top == stk + 64 * S.stack_depth) return;
-#endif
       *top = e;
       top += 64;
     };
@@ -1789,12 +1609,9 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 #ifndef RT_SHADE_MERGE_F
 #define RT_SHADE_MERGE_F(F) (RT_SHADE_MERGE != 0 && ((F) & ~F_BVH4) == 0)
 #endif
-// PRE: the shading event's Philox block was drawn by the caller (rnp: the
-// merged regeneration below draws it together with the camera blocks of the
-// lanes that start new paths).
-template <bool STATS, unsigned F, bool PRE = false>
+template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
-                       const Hit &h, Counters &cnt, const double *rnp = nullptr) {
+                       const Hit &h, Counters &cnt) {
   const uint32_t b = ps.bounce;
   const DMat M = S.mats[h.mat];
   if (STATS) cnt.shade++;
@@ -1807,14 +1624,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     return false;
   }
   double rn[4]; // one block per shading event: (e0, e1, d0, d1)
-  if constexpr (PRE) {
-    rn[0] = rnp[0];
-    rn[1] = rnp[1];
-    rn[2] = rnp[2];
-    rn[3] = rnp[3];
-  } else {
-    u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
-  }
+  u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   constexpr bool kMerge = RT_SHADE_MERGE_F(F);

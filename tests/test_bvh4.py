@@ -121,3 +121,30 @@ def test_bvh4_kept_binary_when_its_stacks_do_not_fit_lds():
     assert ic["lds_fixed_bytes"] <= ic["lds_block_budget"] <= cap
     assert np.array_equal(c, a)  # the same binary tree and walk
     compare(b, a, 1e-12)
+
+
+def test_binary_stacks_over_the_lds_share_still_render():
+    """When even the binary walk's traversal stacks (plus the static LDS)
+    exceed the per-block LDS share at the instance's occupancy target -- a
+    compiler or register change can move that share -- the scene still loads:
+    no BVH nodes are staged and fewer blocks are resident per CU.
+    RTX_LDS_CAP lowers the share below the binary tree's fixed bytes; the
+    image is bit-identical to the uncapped render (same tree, same walk)."""
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    cam = S.camera_desc(image_width=40, samples_per_pixel=4, max_depth=8)
+    f = camera_frame(cam)
+    i2, a, _ = render_arity(S, f, 2, 13)
+    cap = i2["lds_fixed_bytes"] // 2
+    old = os.environ.get("RTX_LDS_CAP")
+    os.environ["RTX_LDS_CAP"] = str(cap)
+    try:
+        ic, c, _ = render_arity(S, f, 2, 13)
+    finally:
+        if old is None:
+            os.environ.pop("RTX_LDS_CAP")
+        else:
+            os.environ["RTX_LDS_CAP"] = old
+    assert ic["bvh_arity"] == 2
+    assert ic["lds_nodes"] == 0
+    assert ic["lds_fixed_bytes"] > ic["lds_block_budget"]
+    assert np.array_equal(c, a)
