@@ -608,10 +608,12 @@ def main():
         shard = TileShardedRenderer(tile_render_fn, frame, rank, ws)
         bufs = [shard.buffer(dev) for _ in range(2)]
         gath = [shard.gather_buffer(dev) if rank == 0 else None for _ in range(2)]
-        tsum = [None, None]  # per-tile sums (chunk sum) of each buffer
+        sums = [shard.sum_buffer(dev) for _ in range(2)]   # per-tile sums (device chunk sum)
+        frames = [shard.frame_buffer(dev) if rank == 0 else None for _ in range(2)]
+        tsum = [None, None]
 
         def launch_work(seed, b):
-            tsum[b] = shard.render(bufs[b], seed)
+            tsum[b] = shard.render(bufs[b], seed, out=sums[b])
     else:
         shard = ShardedRenderer(render_fn, frame, rank, ws)
         assert shard.strata == (s0, s1)
@@ -626,8 +628,9 @@ def main():
             work.wait()
         if rank == 0:
             if tiles_mode:
-                # reorder the gathered tiles (N=1: this rank's own tile sums)
-                final["frame"] = shard.frame_sums(gath[b] if use_pg else tsum[b].unsqueeze(0))
+                # reorder the gathered tiles on the device (N=1: this rank's own tile sums)
+                final["frame"] = shard.frame_sums(gath[b] if use_pg else tsum[b].unsqueeze(0),
+                                                  out=frames[b])
             else:
                 final["frame"] = bufs[b]
             final["step"] = k

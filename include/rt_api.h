@@ -27,6 +27,11 @@
  *                        (src/core/camera/StaticCamera.cpp:136-313) extended to N devices:
  *                        one scene and one host thread per shard, 8x8 tiles dealt
  *                        round-robin over the shards (SURVEY §8(b) "Threading")
+ *   rt_tiles_sum_device / rt_tiles_to_frame_device
+ *                     <- the batch assembly of StaticCamera::render_gpu (the D2H copy of each
+ *                        64-row batch into its rows of the frame, StaticCamera.cpp:281-299) for
+ *                        tile shards: chunk partials summed and tiles reordered into frame rows
+ *                        on the device, before the one copy out
  *   rt_last_error     <- replaces CUDA_CHECK's exit() and the converters' exceptions
  *                        (CudaMemoryUtility.cuh:9-15, HittableConverter.cuh:103-108): errors are
  *                        returned as negative codes, never thrown or exit()ed across the ABI.
@@ -62,8 +67,10 @@ extern "C" {
    any other call (rtx/lib.py does): structs are passed by pointer without a
    size field, so a caller built against another version must not proceed.
    2: rt_scene_desc.bvh_arity, rt_path_stats.cyc_*, rt_scene_info's stack and
-      LDS fields. */
-#define RT_ABI_VERSION 2
+      LDS fields.
+   3: rt_tiles_sum_device, rt_tiles_to_frame_device, rt_multi_gather_ms; the
+      rt_multi exchange runs on the devices. */
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define RT_OK 0
@@ -356,6 +363,26 @@ int rt_last_kernel_ms(rt_scene *scene, double *ms);
 int rt_to_bytes_device(const double *device_rgb, int64_t n_pixels, double scale,
                        uint8_t *device_bytes, void *hip_stream);
 
+/* ---- tile exchange (multi-GPU tile sharding) ------------------------------ */
+/* Tile-layout chunk partials [tile][chunk][64][3] (rt_render_device with
+   RT_LAYOUT_TILES and strata_chunks = chunks) -> per-tile sums [tile][64][3],
+   each added in chunk order on the device.  parts and device_tiles must not
+   overlap (unless chunks == 1). */
+int rt_tiles_sum_device(const double *device_parts, int64_t n_tiles, int32_t chunks,
+                        double *device_tiles, void *hip_stream);
+
+/* Compact tiles of n_shards tile shards -> frame rows on the device: tile t of
+   the row range [params->row_begin, row_end) in row-major tile order (shard
+   t % n_shards rendered it as its local tile t / n_shards) is read from
+   device_tiles[(t % n_shards) * shard_stride + t / n_shards][64][3] and
+   written to device_rgb (index (j-row_begin)*W+i), scaled by
+   pixel_samples_scale when params->output is RT_OUT_SCALED, added when
+   params->accumulate.  shard_stride (tiles) >= ceil(tiles / n_shards): the
+   padded per-shard slot of a gather (RCCL gather into [shard][stride]). */
+int rt_tiles_to_frame_device(const double *device_tiles, int32_t n_shards, int64_t shard_stride,
+                             const rt_frame *frame, const rt_render_params *params,
+                             double *device_rgb, void *hip_stream);
+
 /* ---- multi-device rendering (tile shards) -------------------------------- */
 typedef struct rt_multi rt_multi; /* opaque: one rt_scene per shard */
 
@@ -370,8 +397,10 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
 
 /* rt_render over the shards: shard k renders the 8x8 tiles t = k (mod
    n_shards) of the row range, all launched strata, in (tile, stratum chunk)
-   work units, on its own host thread; the host gathers the tile sums and adds
-   each pixel's chunk partials in chunk order.  params->tile_first/tile_stride/
+   work units, on its own host thread, and adds each of its pixels' chunk
+   partials in chunk order on its device; the compact tiles are copied device
+   to device (xGMI peer copies) to shard 0's device, reordered into the frame
+   there (rt_tiles_to_frame_device's kernel) and copied to host_rgb once.  params->tile_first/tile_stride/
    layout must be 0/0-or-1/RT_LAYOUT_FRAME; params->strata_chunks 0 = the chunk
    split rt_render's frame launch uses on shard 0's device, which makes the
    output bit-identical to rt_render on one device.  Synchronous. */
@@ -381,6 +410,11 @@ int rt_multi_render(rt_multi *multi, const rt_frame *frame, const rt_render_para
 /* Device time (ms) of each shard's last render kernel (HIP events on its
    launch stream); ms must hold n_shards doubles (0 for a shard with no tiles). */
 int rt_multi_shard_ms(rt_multi *multi, double *ms);
+
+/* Host time (ms) of the last rt_multi_render's exchange: from the slowest
+   shard's render completion to the frame assembled on shard 0's device (the
+   peer copies and the reorder; the final D2H copy excluded). */
+int rt_multi_gather_ms(rt_multi *multi, double *ms);
 
 int rt_multi_destroy(rt_multi *multi);
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +47,13 @@ extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *
                                                 hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double scale,
                                           uint8_t *bytes, hipStream_t stream);
+extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
+                                           hipStream_t stream);
+extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
+                                              int n_chunks, double *out, hipStream_t stream);
+extern "C" hipError_t rtk_launch_tiles_to_frame(const double *tiles, int n_shards, int64_t shard_stride,
+                                                int W, int row_begin, int row_end, double scale, int scaled,
+                                                int accumulate, double *out, hipStream_t stream);
 
 struct rt_scene {
   int device = 0;
@@ -840,21 +848,66 @@ int rt_to_bytes_device(const double *rgb, int64_t n, double scale, uint8_t *byte
   return RT_OK;
 }
 
+// ---------------------------------------------------------------- tile exchange
+int rt_tiles_sum_device(const double *parts, int64_t n_tiles, int32_t chunks, double *device_tiles,
+                        void *hip_stream) {
+  if (!parts || !device_tiles || n_tiles < 0 || chunks < 1) return set_err(RT_ERR_INVALID, "invalid argument");
+  if (parts == device_tiles && chunks > 1) return set_err(RT_ERR_INVALID, "parts and tiles must not alias");
+  hipError_t e = rtk_launch_tiles_sum(parts, n_tiles, chunks, device_tiles, (hipStream_t)hip_stream);
+  if (e != hipSuccess) return hip_err(e, "tiles_sum launch");
+  return RT_OK;
+}
+
+int rt_tiles_to_frame_device(const double *device_tiles, int32_t n_shards, int64_t shard_stride,
+                             const rt_frame *f, const rt_render_params *p, double *device_rgb,
+                             void *hip_stream) {
+  if (!device_tiles || !device_rgb || !f || !p || n_shards < 1)
+    return set_err(RT_ERR_INVALID, "invalid argument");
+  DLaunch L;
+  int rc = to_launch(f, p, L);
+  if (rc) return rc;
+  const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
+  if (shard_stride < (n_tiles + n_shards - 1) / n_shards)
+    return set_err(RT_ERR_INVALID, "shard_stride below the tiles of one shard");
+  hipError_t e = rtk_launch_tiles_to_frame(device_tiles, n_shards, shard_stride, f->image_width, L.row_begin,
+                                           L.row_end, f->pixel_samples_scale, p->output == RT_OUT_SCALED,
+                                           p->accumulate, device_rgb, (hipStream_t)hip_stream);
+  if (e != hipSuccess) return hip_err(e, "tiles_to_frame launch");
+  return RT_OK;
+}
+
 // ---------------------------------------------------------------- multi-device
 // One rt_scene per shard, one host thread per shard (StaticCamera::render_gpu's
 // single-device loop, StaticCamera.cpp:136-313, spread over N devices).  Shard
-// k renders tiles k, k+N, k+2N, ... in the compact tile layout; the host adds
-// each pixel's chunk partials in chunk order -- the order split_sum_kernel
-// uses -- so with the frame launch's chunk split the frame is bit-identical to
-// rt_render on one device.
+// k renders tiles k, k+N, k+2N, ... in the compact tile layout and finishes
+// them on its own device (shard_finish_kernel: chunk partials added in chunk
+// order -- split_sum_kernel's order); the compact tiles travel device to
+// device (xGMI peer copies) into a staging buffer on shard 0's device, where
+// tiles_to_frame_kernel reorders them into the frame, copied to the host once.
+// With the frame launch's chunk split the frame is bit-identical to rt_render
+// on one device.
 struct rt_multi {
-  std::vector<rt_scene *> scenes; // one per shard
-  std::vector<std::vector<double>> parts;
+  std::vector<rt_scene *> scenes; // one per shard; scenes[0]'s device is the root
   std::vector<double> ms;
+  double gather_ms = 0.0;
+  double *stage = nullptr; // root device: [shard][stride tiles][64][3]
+  size_t stage_bytes = 0;
+  double *frame = nullptr; // root device: the assembled rows
+  size_t frame_bytes = 0;
 };
 
 int rt_multi_destroy(rt_multi *m) {
   if (!m) return RT_OK;
+  if (!m->scenes.empty() && m->scenes[0]) {
+    DeviceGuard g(m->scenes[0]->device);
+    for (rt_scene *s : m->scenes)
+      if (s) {
+        DeviceGuard gs(s->device);
+        (void)hipStreamSynchronize(s->stream);
+      }
+    if (m->stage) (void)hipFree(m->stage);
+    if (m->frame) (void)hipFree(m->frame);
+  }
   for (rt_scene *s : m->scenes) rt_scene_destroy(s);
   delete m;
   return RT_OK;
@@ -874,7 +927,6 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
   std::vector<std::string> err(n_shards);
   try {
     m->scenes.assign(n_shards, nullptr);
-    m->parts.resize(n_shards);
     m->ms.assign(n_shards, 0.0);
     std::vector<std::thread> th;
     try {
@@ -898,18 +950,31 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
       rt_multi_destroy(m);
       return set_err(rc[k], "shard " + std::to_string(k) + ": " + err[k]);
     }
+  // direct xGMI access from every shard device to the root's memory (where
+  // the peer copies land); without it hipMemcpyPeerAsync stages through the host
+  const int root = devices[0];
+  for (int d = 1; d < n_devices && d < n_shards; ++d) {
+    if (devices[d] == root) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, devices[d], root) == hipSuccess && can) {
+      DeviceGuard g(devices[d]);
+      hipError_t e = hipDeviceEnablePeerAccess(root, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    }
+  }
   *out = m;
   return RT_OK;
 }
 
 // One shard of rt_multi_render: the tiles t = first + k * stride in the tile
 // layout with the one-device frame's split plan -- tiles below plan.n_head
-// (global index) as head units, the rest as tail chunks -- raw sums: whole
-// head tiles' [k][64][3] into `whole`, the chunk partials (the launch's parts
-// layout) into `parts` (host buffers, resized here).
-static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *p, int first,
-                        int stride, const SplitPlan &plan, SplitPlan *local,
-                        std::vector<double> &whole, std::vector<double> &parts) {
+// (global index) as head units, the rest as tail chunks -- raw sums, finished
+// on the shard's device into its compact tiles [k][64][3] (whole head tiles
+// by their own units, chunked tiles by shard_finish_kernel), then copied into
+// the root's staging slot `dst`.  *t_done: host clock (ms) when the render and
+// finish kernels had completed.
+static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *p, int first, int stride,
+                        const SplitPlan &plan, double *dst, int root_dev, double *t_done) {
   DCamera C;
   DLaunch L;
   rt_render_params q = *p;
@@ -924,24 +989,22 @@ static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *
   if ((rc = to_launch(f, &q, L))) return rc;
   SplitPlan sp = plan;
   sp.n_head = plan.n_head > first ? std::min(L.n_local_tiles, (plan.n_head - first + stride - 1) / stride) : 0;
-  *local = sp;
   DeviceGuard g(s->device);
-  const size_t nw = sp.head_chunks == 1 ? (size_t)sp.n_head * 64 * 3 : 0;
-  const size_t np = plan_parts(sp, L.n_local_tiles) * 64 * 3;
-  try {
-    whole.resize(nw);
-    parts.resize(np);
-  } catch (const std::exception &) {
-    return set_err(RT_ERR_OOM, "host tile buffers");
-  }
-  if ((rc = ensure_out(s, std::max<size_t>(nw, 1) * sizeof(double)))) return rc;
+  const size_t nt = (size_t)L.n_local_tiles * 64 * 3;
+  if ((rc = ensure_out(s, std::max<size_t>(nt, 1) * sizeof(double)))) return rc;
   if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream, &sp))) return rc;
-  hipError_t e = hipSuccess;
-  if (nw) e = hipMemcpyAsync(whole.data(), s->out_buf, nw * sizeof(double), hipMemcpyDeviceToHost, s->stream);
-  if (e == hipSuccess && np)
-    e = hipMemcpyAsync(parts.data(), s->scratch, np * sizeof(double), hipMemcpyDeviceToHost, s->stream);
+  hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
+                                         s->out_buf, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return hip_err(e, "shard render");
+  *t_done = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  if (nt) {
+    e = s->device == root_dev
+            ? hipMemcpyAsync(dst, s->out_buf, nt * sizeof(double), hipMemcpyDeviceToDevice, s->stream)
+            : hipMemcpyPeerAsync(dst, root_dev, s->out_buf, s->device, nt * sizeof(double), s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) return hip_err(e, "shard tiles to the root device");
+  }
   return RT_OK;
 }
 
@@ -950,36 +1013,58 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   if (p->tile_first != 0 || p->tile_stride > 1 || p->layout != RT_LAYOUT_FRAME)
     return set_err(RT_ERR_INVALID, "rt_multi_render takes a whole-frame launch "
                                    "(tile_first 0, tile_stride 0/1, RT_LAYOUT_FRAME)");
-  DCamera C;
   DLaunch L;
-  int rc = to_device_camera(f, C);
-  if (rc) return rc;
   rt_render_params full = *p;
   full.strata_chunks = 0;
-  if ((rc = to_launch(f, &full, L))) return rc;
+  full.accumulate = 0;
+  int rc = to_launch(f, &full, L);
+  if (rc) return rc;
   const int n = (int)m->scenes.size();
+  rt_scene *root = m->scenes[0];
   // the one-device frame launch's units (so the frame is bit-identical to
   // rt_render on one device), or every tile in strata_chunks chunks if asked
-  SplitPlan plan = frame_plan(m->scenes[0], L);
+  SplitPlan plan = frame_plan(root, L);
   if (p->strata_chunks > 0)
     plan = SplitPlan{0, 1, std::max(1, std::min(p->strata_chunks, std::max(1, L.sample_count)))};
-  const int W = f->image_width, r0 = L.row_begin, r1 = L.row_end;
   const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
+  const int64_t stride = (n_tiles + n - 1) / n; // staging slot per shard, in tiles
+  const size_t frame_d = (size_t)(L.row_end - L.row_begin) * f->image_width * 3;
+  {
+    DeviceGuard g(root->device);
+    auto grow = [&](double *&buf, size_t &have, size_t bytes, const char *what) -> int {
+      if (have >= bytes) return RT_OK;
+      if (buf) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(buf);
+        buf = nullptr;
+        have = 0;
+      }
+      hipError_t e = hipMalloc((void **)&buf, bytes);
+      if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc ") + what + ": " + hipGetErrorString(e));
+      have = bytes;
+      return RT_OK;
+    };
+    if ((rc = grow(m->stage, m->stage_bytes, std::max<size_t>(1, (size_t)n * stride * 64 * 3) * sizeof(double),
+                   "multi staging")))
+      return rc;
+    if ((rc = grow(m->frame, m->frame_bytes, std::max<size_t>(1, frame_d) * sizeof(double), "multi frame")))
+      return rc;
+  }
   std::vector<int> src(n, RT_OK);
-  std::vector<SplitPlan> lp(n, plan);
+  std::vector<double> t_done(n, 0.0);
   std::vector<std::string> err(n);
-  std::vector<std::vector<double>> whole(n);
   std::vector<std::thread> th;
   try {
-  for (int k = 0; k < n; ++k) {
-    m->ms[k] = 0.0;
-    if (k >= n_tiles) continue; // more shards than tiles
-    th.emplace_back([&, k]() {
-      src[k] = render_shard(m->scenes[k], f, p, k, n, plan, &lp[k], whole[k], m->parts[k]);
-      if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
-      if (src[k] != RT_OK) err[k] = g_err;
-    });
-  }
+    for (int k = 0; k < n; ++k) {
+      m->ms[k] = 0.0;
+      if (k >= n_tiles) continue; // more shards than tiles
+      th.emplace_back([&, k]() {
+        src[k] = render_shard(m->scenes[k], f, p, k, n, plan, m->stage + (size_t)k * stride * 64 * 3,
+                              root->device, &t_done[k]);
+        if (src[k] == RT_OK) src[k] = rt_last_kernel_ms(m->scenes[k], &m->ms[k]);
+        if (src[k] != RT_OK) err[k] = g_err;
+      });
+    }
   } catch (const std::exception &ex) { // thread creation failed: join the started ones
     for (auto &t : th) t.join();
     return set_err(RT_ERR_DEVICE, std::string("shard thread: ") + ex.what());
@@ -987,43 +1072,30 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
   for (auto &t : th) t.join();
   for (int k = 0; k < n; ++k)
     if (src[k] != RT_OK) return set_err(src[k], "shard " + std::to_string(k) + ": " + err[k]);
-  // gather: tile t = k + lt*n of shard k; pixel (x, y) of the tile at slot
-  // y*8+x; a chunked tile's partials added in chunk order (split_sum_kernel's)
-  const bool scaled = p->output == RT_OUT_SCALED;
-  for (int k = 0; k < n && k < n_tiles; ++k) {
-    const SplitPlan &sp = lp[k];
-    const double *wh = whole[k].data(), *part = m->parts[k].data();
-    for (int64_t t = k, lt = 0; t < n_tiles; t += n, ++lt) {
-      const int tx = (int)(t % L.tiles_x), ty = (int)(t / L.tiles_x);
-      const bool head = lt < sp.n_head, is_whole = head && sp.head_chunks == 1;
-      const int nc = head ? sp.head_chunks : sp.chunks;
-      const int64_t part0 = head ? lt * nc
-                                 : (sp.head_chunks > 1 ? (int64_t)sp.n_head * sp.head_chunks : 0) +
-                                       (lt - sp.n_head) * nc;
-      for (int slot = 0; slot < 64; ++slot) {
-        const int i = tx * 8 + (slot & 7), j = r0 + ty * 8 + (slot >> 3);
-        if (i >= W || j >= r1) continue;
-        double *o = host_rgb + 3 * ((size_t)(j - r0) * W + i);
-        for (int ch = 0; ch < 3; ++ch) {
-          double sum;
-          if (is_whole) {
-            sum = wh[((size_t)lt * 64 + slot) * 3 + ch];
-          } else {
-            const double *pp = part + ((size_t)part0 * 64 + slot) * 3 + ch;
-            sum = pp[0];
-            for (int c = 1; c < nc; ++c) sum += pp[(size_t)c * 64 * 3];
-          }
-          o[ch] = scaled ? C.scale * sum : sum;
-        }
-      }
-    }
-  }
+  DeviceGuard g(root->device);
+  hipError_t e = rtk_launch_tiles_to_frame(m->stage, n, stride, f->image_width, L.row_begin, L.row_end,
+                                           f->pixel_samples_scale, p->output == RT_OUT_SCALED, 0, m->frame,
+                                           root->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(root->stream);
+  if (e != hipSuccess) return hip_err(e, "tiles_to_frame");
+  const double t_frame =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  m->gather_ms = t_frame - *std::max_element(t_done.begin(), t_done.end());
+  e = hipMemcpyAsync(host_rgb, m->frame, frame_d * sizeof(double), hipMemcpyDeviceToHost, root->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(root->stream);
+  if (e != hipSuccess) return hip_err(e, "frame D2H");
   return RT_OK;
 }
 
 int rt_multi_shard_ms(rt_multi *m, double *ms) {
   if (!m || !ms) return set_err(RT_ERR_INVALID, "null argument");
   for (size_t k = 0; k < m->ms.size(); ++k) ms[k] = m->ms[k];
+  return RT_OK;
+}
+
+int rt_multi_gather_ms(rt_multi *m, double *ms) {
+  if (!m || !ms) return set_err(RT_ERR_INVALID, "null argument");
+  *ms = m->gather_ms;
   return RT_OK;
 }
 

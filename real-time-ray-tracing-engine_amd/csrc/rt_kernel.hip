@@ -463,6 +463,64 @@ __global__ void split_sum_kernel(const double *parts, DCamera C, DLaunch P, doub
   *o = P.accumulate ? *o + sum : sum;
 }
 
+// ---- tile-shard exchange (multi-GPU: rt_multi_render, rtx/dist.py) ----
+// Every kernel below adds chunk partials in chunk order (split_sum_kernel's
+// order), so a sharded frame is bit-identical to the one-device frame launch.
+// A tile's record is 64 pixel slots x 3 channels = 192 doubles; one thread per
+// double, consecutive threads on consecutive doubles (coalesced).
+constexpr int kTileD = 64 * 3;
+
+// Tile-layout chunk partials [tile][chunk][64][3] -> tile sums [tile][64][3].
+__global__ void tiles_sum_kernel(const double *parts, int64_t n_tiles, int chunks, double *out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_tiles * kTileD) return;
+  const int64_t tile = idx / kTileD, r = idx - tile * kTileD;
+  const double *p = parts + tile * chunks * kTileD + r;
+  double sum = p[0];
+  for (int c = 1; c < chunks; ++c) sum += p[(int64_t)c * kTileD];
+  out[idx] = sum;
+}
+
+// One shard's compact tiles finished on its own device: its whole head tiles
+// are already in out[lt]; each chunked tile's partials (the launch's parts
+// layout, DLaunch) are summed in chunk order into out[lt].
+__global__ void shard_finish_kernel(const double *parts, int n_local, int n_head, int head_chunks,
+                                    int n_chunks, double *out) {
+  const int first = head_chunks > 1 ? 0 : n_head; // first chunked local tile
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)(n_local - first) * kTileD) return;
+  const int lt = first + (int)(idx / kTileD);
+  const int r = (int)(idx % kTileD);
+  const bool head = lt < n_head;
+  const int nc = head ? head_chunks : n_chunks;
+  const int64_t part0 = head ? (int64_t)lt * nc
+                             : (head_chunks > 1 ? (int64_t)n_head * head_chunks : 0) + (int64_t)(lt - n_head) * nc;
+  const double *p = parts + part0 * kTileD + r;
+  double sum = p[0];
+  for (int c = 1; c < nc; ++c) sum += p[(int64_t)c * kTileD];
+  out[(int64_t)lt * kTileD + r] = sum;
+}
+
+// Compact tiles of n_shards shards -> frame rows [row_begin, row_end): tile t
+// of the row range (row-major tile order) is local tile t / n_shards of shard
+// t % n_shards, at tiles[(shard * shard_stride + local) * 192].  One thread per
+// frame double: the frame writes are coalesced, the tile reads come in runs
+// of 8 pixels (192 B).
+__global__ void tiles_to_frame_kernel(const double *tiles, int n_shards, int64_t shard_stride, int W,
+                                      int row_begin, int row_end, int tiles_x, double scale, int scaled,
+                                      int accumulate, double *out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)(row_end - row_begin) * W * 3) return;
+  const int ch = (int)(idx % 3);
+  const int64_t pix = idx / 3;
+  const int i = (int)(pix % W), jr = (int)(pix / W);
+  const int t = (jr >> 3) * tiles_x + (i >> 3), slot = (jr & 7) * 8 + (i & 7);
+  const int k = t % n_shards, lt = t / n_shards;
+  double v = tiles[((int64_t)k * shard_stride + lt) * kTileD + slot * 3 + ch];
+  if (scaled) v = scale * v;
+  out[idx] = accumulate ? out[idx] + v : v;
+}
+
 __global__ void to_bytes_kernel(const double *rgb, int64_t n, double scale, uint8_t *bytes) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 3 * n) return;
@@ -659,6 +717,36 @@ extern "C" hipError_t rtk_launch_render_chunked(const DScene *S, const DCamera *
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                      scratch, *C, Q, out);
+  return hipGetLastError();
+}
+
+static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
+                                           hipStream_t stream) {
+  if (n_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tiles_sum_kernel, dim3(blocks_for(n_tiles * kTileD)), dim3(256), 0, stream, parts,
+                     n_tiles, chunks, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
+                                              int n_chunks, double *out, hipStream_t stream) {
+  const int first = head_chunks > 1 ? 0 : n_head;
+  const int64_t total = (int64_t)(n_local - first) * kTileD;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(shard_finish_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, parts, n_local,
+                     n_head, head_chunks, n_chunks, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_tiles_to_frame(const double *tiles, int n_shards, int64_t shard_stride,
+                                                int W, int row_begin, int row_end, double scale, int scaled,
+                                                int accumulate, double *out, hipStream_t stream) {
+  const int64_t total = (int64_t)(row_end - row_begin) * W * 3;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tiles_to_frame_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, tiles, n_shards,
+                     shard_stride, W, row_begin, row_end, (W + 7) / 8, scale, scaled, accumulate, out);
   return hipGetLastError();
 }
 

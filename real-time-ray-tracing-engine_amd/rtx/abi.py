@@ -5,7 +5,7 @@ sizes against the compiled library's own view (rt_abi_sizes) when available.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 2  # include/rt_api.h; rtx/lib.py refuses a library of another version
+RT_ABI_VERSION = 3  # include/rt_api.h; rtx/lib.py refuses a library of another version
 
 RT_OK = 0
 RT_ERR_INVALID = -1
@@ -127,5 +127,5 @@ EXPORTS = (
     "rt_scene_create", "rt_scene_info_get", "rt_scene_destroy", "rt_render",
     "rt_render_device", "rt_render_stats", "rt_last_kernel_ms", "rt_to_bytes_device",
     "rt_multi_create", "rt_multi_render", "rt_multi_shard_ms", "rt_multi_destroy",
-    "rt_scene_bvh_cost",
+    "rt_scene_bvh_cost", "rt_tiles_sum_device", "rt_tiles_to_frame_device", "rt_multi_gather_ms",
 )

@@ -5,8 +5,11 @@ Two decompositions of one frame over the ranks of the default process group:
 * tile sharding (default in bench.py): the frame's 8x8 tiles are dealt out
   round-robin, tile t to rank t % world, so cheap (sky) and expensive tiles
   spread evenly; each rank renders ALL strata of its tiles into a compact tile
-  buffer (RT_LAYOUT_TILES) and rank 0 gathers the buffers (1/world of the frame
-  from each rank, over all of rank 0's xGMI links at once) and reorders them.
+  buffer (RT_LAYOUT_TILES), adds each tile's chunk partials on its device
+  (rt_tiles_sum_device), and rank 0 gathers the tile sums (1/world of the frame
+  from each rank, over all of rank 0's xGMI links at once) and reorders them
+  into the frame on its device (rt_tiles_to_frame_device): the timed region
+  runs library kernels and the RCCL gather, no framework ops.
   Every pixel is computed by exactly one GPU.  Its strata are split into the
   rank's own chunk count (`auto_chunks`, sized for each rank's wave slots), not
   the one-GPU frame launch's, so a pixel's chunk partials are added in a
@@ -26,10 +29,13 @@ gloo for the CPU tests.  The counter-based RNG is keyed by the global stratum
 index, so the union of the shards is exactly the one-GPU sample set: the result
 equals a single-GPU render up to fp64 summation order.
 """
+import ctypes as C
 import os
 
 import torch
 import torch.distributed as dist
+
+from . import abi
 
 
 def strata_shard(n_strata, rank, world):
@@ -76,15 +82,35 @@ def tile_counts(frame, world):
     return n, (n + world - 1) // world
 
 
-def tiles_to_frame(gathered, width, height):
-    """Gathered compact tile buffers [world, T_r, 64, 3] (rank r holds tiles
-    r, r + world, r + 2*world, ... in RT_LAYOUT_TILES order) -> frame [H, W, 3]."""
-    world, t_r = gathered.shape[0], gathered.shape[1]
-    tx, ty = (width + 7) // 8, (height + 7) // 8
-    n = tx * ty
-    flat = gathered.transpose(0, 1).reshape(t_r * world, 64, gathered.shape[-1])[:n]
-    img = flat.reshape(ty, tx, 8, 8, -1).permute(0, 2, 1, 3, 4).reshape(ty * 8, tx * 8, -1)
-    return img[:height, :width]
+def _stream_of(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def device_tiles_sum(parts, out):
+    """Chunk partials [T, chunks, 64, 3] -> tile sums `out` [T, 64, 3] on the
+    device (rt_tiles_sum_device: chunk order, the one-GPU frame launch's
+    summation order), on the tensors' current stream."""
+    from .lib import check, load
+    assert parts.is_cuda and out.is_cuda and parts.is_contiguous() and out.is_contiguous()
+    assert parts.dtype == out.dtype == torch.float64 and out.shape == (parts.shape[0], 64, 3)
+    check(load().rt_tiles_sum_device(C.c_void_p(parts.data_ptr()), parts.shape[0], parts.shape[1],
+                                     C.c_void_p(out.data_ptr()), C.c_void_p(_stream_of(out))))
+    return out
+
+
+def device_tiles_to_frame(gathered, frame, out):
+    """Gathered compact tile sums [world, T_r, 64, 3] (rank r holds tiles r,
+    r + world, ... in RT_LAYOUT_TILES order) -> the frame's raw sums `out`
+    [H, W, 3] on the device (rt_tiles_to_frame_device)."""
+    from .lib import check, load
+    from .render import Renderer
+    assert gathered.is_cuda and out.is_cuda and gathered.is_contiguous() and out.is_contiguous()
+    assert out.shape == (frame.image_height, frame.image_width, 3)
+    p = Renderer.params(output=abi.RT_OUT_SUM)
+    check(load().rt_tiles_to_frame_device(C.c_void_p(gathered.data_ptr()), gathered.shape[0],
+                                          gathered.shape[1], C.byref(frame), C.byref(p),
+                                          C.c_void_p(out.data_ptr()), C.c_void_p(_stream_of(out))))
+    return out
 
 
 def auto_chunks(frame, world, target_units=None):
@@ -108,28 +134,43 @@ class TileShardedRenderer:
     `buf` ([T_r, chunks, 64, 3] float64) with the raw sums of all strata of
     those tiles in RT_LAYOUT_TILES order, each tile's strata split into
     `chunks` (Renderer.render_device with output=RT_OUT_SUM, accumulate=0,
-    layout=RT_LAYOUT_TILES, chunks=chunks)."""
+    layout=RT_LAYOUT_TILES, chunks=chunks).  The chunk sum and the tile ->
+    frame reorder are the library's device kernels (tiles_sum(parts, out),
+    to_frame(gathered, frame, out)); the CPU tests pass torch equivalents for
+    their host tensors."""
 
-    def __init__(self, render_fn, frame, rank=0, world=1, chunks=None):
+    def __init__(self, render_fn, frame, rank=0, world=1, chunks=None, tiles_sum=None,
+                 to_frame=None):
         self.render_fn = render_fn
         self.frame = frame
         self.rank, self.world = rank, world
         self.n_tiles, self.tiles_per_rank = tile_counts(frame, world)
         self.chunks = auto_chunks(frame, world) if chunks is None else max(1, chunks)
+        self.tiles_sum = tiles_sum or device_tiles_sum
+        self.to_frame = to_frame or device_tiles_to_frame
 
     def buffer(self, device=None):
         return torch.zeros((self.tiles_per_rank, self.chunks, 64, 3), dtype=torch.float64,
                            device=device)
 
+    def sum_buffer(self, device=None):
+        return torch.zeros((self.tiles_per_rank, 64, 3), dtype=torch.float64, device=device)
+
     def gather_buffer(self, device=None):
         return torch.zeros((self.world, self.tiles_per_rank, 64, 3), dtype=torch.float64,
                            device=device)
 
-    def render(self, buf, seed):
+    def frame_buffer(self, device=None):
+        return torch.zeros((self.frame.image_height, self.frame.image_width, 3),
+                           dtype=torch.float64, device=device)
+
+    def render(self, buf, seed, out=None):
         """Render this rank's tiles; returns the per-tile sums [T_r, 64, 3] (the
-        chunk sum, in fixed chunk order)."""
+        chunk sum, in fixed chunk order) in `out` (a sum_buffer)."""
         self.render_fn(self.frame, buf, seed, (self.rank, self.world), self.chunks)
-        return buf[:, 0] if self.chunks == 1 else buf.sum(dim=1)
+        if self.chunks == 1:
+            return buf[:, 0]
+        return self.tiles_sum(buf, out if out is not None else self.sum_buffer(buf.device))
 
     def gather(self, tiles, gathered=None, async_op=False):
         """Collect every rank's [T_r, 64, 3] tile sums on rank 0 (gathered:
@@ -140,8 +181,10 @@ class TileShardedRenderer:
         parts = list(gathered.unbind(0)) if self.rank == 0 else None
         return dist.gather(tiles.contiguous(), gather_list=parts, dst=0, async_op=async_op)
 
-    def frame_sums(self, gathered):
-        return tiles_to_frame(gathered, self.frame.image_width, self.frame.image_height)
+    def frame_sums(self, gathered, out=None):
+        """The frame's raw sums [H, W, 3] from the gathered tile sums."""
+        return self.to_frame(gathered, self.frame,
+                             out if out is not None else self.frame_buffer(gathered.device))
 
     def step(self, buf, gathered, seed):
         tiles = self.render(buf, seed)

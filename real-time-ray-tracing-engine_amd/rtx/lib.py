@@ -55,6 +55,10 @@ def load():
     L.rt_multi_shard_ms.argtypes = [C.c_void_p, P(C.c_double)]
     L.rt_multi_destroy.argtypes = [C.c_void_p]
     L.rt_scene_bvh_cost.argtypes = [C.c_void_p, P(C.c_double)]
+    L.rt_tiles_sum_device.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p]
+    L.rt_tiles_to_frame_device.argtypes = [C.c_void_p, C.c_int32, C.c_int64, P(abi.Frame),
+                                           P(abi.RenderParams), C.c_void_p, C.c_void_p]
+    L.rt_multi_gather_ms.argtypes = [C.c_void_p, P(C.c_double)]
     for name in abi.EXPORTS:
         getattr(L, name).restype = C.c_char_p if name == "rt_last_error" else C.c_int
     if L.rt_abi_version() != abi.RT_ABI_VERSION:

@@ -178,6 +178,13 @@ class MultiRenderer:
         check(self.lib.rt_multi_shard_ms(self.handle, ms))
         return list(ms)
 
+    def gather_ms(self):
+        """Host ms of the last render's device exchange (slowest shard's render
+        end -> frame assembled on shard 0's device; D2H excluded)."""
+        ms = C.c_double()
+        check(self.lib.rt_multi_gather_ms(self.handle, C.byref(ms)))
+        return ms.value
+
 
 def render_ppm(scene, path, device=0, seed=0, **cam_overrides):
     """StaticCamera::render on the HIP path: camera setup, render, PPM."""

@@ -76,7 +76,34 @@ def test_two_rank_gloo_frame_equals_single_process(tmp_path):
 
 
 # ---------------------------------------------------------------- tile sharding
-from rtx.dist import TileShardedRenderer, tile_counts, tiles_to_frame  # noqa: E402
+from rtx.dist import TileShardedRenderer, tile_counts  # noqa: E402
+
+
+def tiles_to_frame(gathered, width, height):
+    """Torch reference of the tile -> frame reorder (the checker of
+    rt_tiles_to_frame_device, and the reorder of the CPU gloo tests):
+    gathered [world, T_r, 64, 3], rank r holding tiles r, r + world, ..."""
+    world, t_r = gathered.shape[0], gathered.shape[1]
+    tx, ty = (width + 7) // 8, (height + 7) // 8
+    n = tx * ty
+    flat = gathered.transpose(0, 1).reshape(t_r * world, 64, gathered.shape[-1])[:n]
+    img = flat.reshape(ty, tx, 8, 8, -1).permute(0, 2, 1, 3, 4).reshape(ty * 8, tx * 8, -1)
+    return img[:height, :width]
+
+
+def tiles_sum(parts, out):
+    """Torch reference of rt_tiles_sum_device: chunk partials added in chunk
+    order (sequentially, so bit for bit the device kernel's order)."""
+    acc = parts[:, 0].clone()
+    for c in range(1, parts.shape[1]):
+        acc = acc + parts[:, c]
+    out.copy_(acc)
+    return out
+
+
+def torch_to_frame(gathered, frame, out):
+    out.copy_(tiles_to_frame(gathered, frame.image_width, frame.image_height))
+    return out
 
 
 def frame_to_tiles(img, first, stride):
@@ -129,7 +156,8 @@ def _tile_worker(rank, world, port, out_path):
                 tl = frame_to_tiles(parts[c], tiles[0], tiles[1])
                 buf[:len(tl), c] = torch.from_numpy(tl)
 
-        tr = TileShardedRenderer(render_fn, frame, rank, world, chunks=chunks)
+        tr = TileShardedRenderer(render_fn, frame, rank, world, chunks=chunks, tiles_sum=tiles_sum,
+                                 to_frame=torch_to_frame)
         buf, g = tr.buffer(), tr.gather_buffer()
         img = tr.step(buf, g, seed=3)
         if rank == 0:
@@ -181,6 +209,55 @@ def test_gpu_tile_layout_reassembles_bit_exact():
         one = R.render(f, seed=6, output=abi.RT_OUT_SUM, tiles=(1, world),
                        layout=abi.RT_LAYOUT_TILES)
     np.testing.assert_allclose(ch.sum(axis=1), one, rtol=1e-12, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_device_tile_exchange_kernels_match_torch():
+    """rt_tiles_sum_device and rt_tiles_to_frame_device (the N>1 path's chunk
+    sum and tile -> frame reorder, rtx/dist.py) against the torch references
+    above, bit for bit, on ragged frames, several worlds, padded shard slots,
+    with scaling and accumulation."""
+    from rtx.dist import device_tiles_sum, device_tiles_to_frame
+    from rtx.lib import check, load
+    from rtx.render import Renderer, camera_frame
+    import ctypes as C
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(5)
+    S = load_scene(SCENE)
+    for width, world, chunks in [(27, 3, 5), (64, 1, 2), (40, 4, 1), (1920, 8, 7)]:
+        f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=4, max_depth=6))
+        n, t_r = tile_counts(f, world)
+        parts = torch.randn((t_r, chunks, 64, 3), generator=g, dtype=torch.float64)
+        want = tiles_sum(parts, torch.empty((t_r, 64, 3), dtype=torch.float64))
+        got = device_tiles_sum(parts.to(dev), torch.empty((t_r, 64, 3), dtype=torch.float64,
+                                                          device=dev))
+        assert torch.equal(got.cpu(), want), (width, world, chunks)
+        gath = torch.randn((world, t_r, 64, 3), generator=g, dtype=torch.float64)
+        want = tiles_to_frame(gath, f.image_width, f.image_height)
+        out = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
+        got = device_tiles_to_frame(gath.to(dev), f, out)
+        assert torch.equal(got.cpu(), want), (width, world)
+        # a row band (its tiles numbered from row r0), scaled, accumulated into
+        # the buffer, read from padded shard slots (stride T_r + 3)
+        r0, r1 = (8 if f.image_height > 16 else 0), f.image_height
+        nb, tb = tile_counts(f, 1)[0], ((f.image_width + 7) // 8) * ((r1 - r0 + 7) // 8)
+        assert tb <= nb
+        slots = torch.zeros((world, t_r + 3, 64, 3), dtype=torch.float64)
+        slots[:, :t_r] = gath
+        base = torch.randn((r1 - r0, f.image_width, 3), generator=g, dtype=torch.float64)
+        want = base + f.pixel_samples_scale * tiles_to_frame(gath, f.image_width, r1 - r0)
+        o = base.to(dev)
+        p = Renderer.params(rows=(r0, r1), output=abi.RT_OUT_SCALED, accumulate=1)
+        check(load().rt_tiles_to_frame_device(C.c_void_p(slots.to(dev).data_ptr()), world, t_r + 3,
+                                              C.byref(f), C.byref(p), C.c_void_p(o.data_ptr()),
+                                              C.c_void_p(0)))
+        torch.cuda.synchronize()
+        assert torch.equal(o.cpu(), want), (width, world, "band")
+    L = load()
+    assert L.rt_tiles_sum_device(None, 1, 1, None, None) == abi.RT_ERR_INVALID
+    x = torch.zeros((2, 2, 64, 3), dtype=torch.float64, device=dev)
+    assert L.rt_tiles_sum_device(C.c_void_p(x.data_ptr()), 2, 2, C.c_void_p(x.data_ptr()),
+                                 None) == abi.RT_ERR_INVALID  # aliasing
 
 
 # ------------------------------------------------------ bench.py N>1 diagnostics

@@ -132,3 +132,25 @@ def test_multi_render_head_tail_plan_bit_identical(scene, spp):
         with MultiRenderer(S, devices=(0,), shards=shards) as M:
             got = M.render(f, seed=4)
         assert np.array_equal(got, one), (shards, np.abs(got - one).max())
+
+
+@pytest.mark.gpu
+def test_multi_render_device_exchange_c2_1080p():
+    """The exchange runs on the devices: each shard adds
+    its chunk partials on its own device, the compact tiles are copied device
+    to device to shard 0's device and reordered there, and the frame leaves
+    the device once.  At C2's 1080p frame (spp 4 keeps the test short; the
+    exchange moves the same 49.8 MB at any spp) with 8 virtual shards on one
+    GPU the frame is bit-identical to one device and the exchange -- slowest
+    shard's render end to the frame assembled on shard 0's device -- is far
+    below a frame time (measured at spp 64 by tools/multi_gather.py)."""
+    S = load_scene(os.path.join(SCENES, "three_spheres.json"))
+    f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=4, max_depth=8))
+    with Renderer(S, device=0) as R:
+        one = R.render(f, seed=12)
+    with MultiRenderer(S, devices=(0,), shards=8) as M:
+        for _ in range(2):
+            got = M.render(f, seed=12)
+        assert np.array_equal(got, one)
+        g = M.gather_ms()
+    assert 0.0 < g < 5.0, g
