@@ -980,6 +980,73 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
   h0 = slab_hit(q, lo0, hi0, tmin32, cl32, t0);
   h1 = slab_hit(q, lo1, hi1, tmin32, cl32, t1);
 }
+// Both children of a binary node staged in LDS, with the planes picked by the
+// ray's direction signs (RT_SLAB_SIGN): for an axis with 1/d >= 0 the lo plane
+// gives the entry distance and the hi plane the exit, the other way round for
+// 1/d < 0 -- fma(plane, 1/d, -P) is monotone in the plane for a fixed 1/d, and
+// every operand is finite (1/d and P are clamped, ray_f32), so min / max of
+// the two plane distances ARE these picks, value for value.  Each lane reads
+// its near and far plane pairs (both children, 8 B) at per-ray byte offsets
+// `po` into the node (lo[a][*] at 8a, hi[a][*] at 24 + 8a): six 8-B LDS reads
+// instead of the twelve planes, and no min / max per plane pair -- the visit
+// drops from 36 to 24 slab VALU plus the six read addresses.
+#ifndef RT_SLAB_SIGN
+#define RT_SLAB_SIGN 1
+#endif
+struct PlaneOff { // per-ray byte offsets of the near plane pair of each axis in a DNode
+  int n[3];
+};
+RT_HD RT_FI PlaneOff plane_offsets(const RayF<true> &q) {
+  PlaneOff o;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) o.n[a] = 8 * a + (q.inv[a] < 0.0f ? 24 : 0);
+  return o;
+}
+RT_HD RT_FI float max3f(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return fmaxf(fmaxf(a, b), c);
+#endif
+}
+RT_HD RT_FI float min3f(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return fminf(fminf(a, b), c);
+#endif
+}
+RT_HD RT_FI void slab_hit2_signed(const RayF<true> &q, const PlaneOff &po, const RT_LDS DNode *node,
+                                  float tmin32, float cl32, float &t0, float &t1, bool &h0, bool &h1) {
+  const RT_LDS char *b = (const RT_LDS char *)node;
+  float nr[3][2], fr[3][2];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const RT_LDS float *pn = (const RT_LDS float *)(b + po.n[a]);
+    const RT_LDS float *pf = (const RT_LDS float *)(b + (16 * a + 24 - po.n[a]));
+    nr[a][0] = pn[0];
+    nr[a][1] = pn[1];
+    fr[a][0] = pf[0];
+    fr[a][1] = pf[1];
+  }
+  float tl[2], th[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float ax = fmaf(nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(fr[0][c], q.inv[0], -q.p[0]);
+    const float ay = fmaf(nr[1][c], q.inv[1], -q.p[1]), by = fmaf(fr[1][c], q.inv[1], -q.p[1]);
+    const float az = fmaf(nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(fr[2][c], q.inv[2], -q.p[2]);
+    tl[c] = max3f(ax, ay, fmaxf(az, tmin32));
+    th[c] = min3f(bx, by, min3f(bz, cl32, cl32));
+  }
+  t0 = tl[0];
+  t1 = tl[1];
+  h0 = tl[0] <= fmaf(th[0], kSlabGrow, q.slack);
+  h1 = tl[1] <= fmaf(th[1], kSlabGrow, q.slack);
+}
 // f32_up(x) as a canonical float (the min/max operations take it as is
 // instead of re-canonicalising it at every box test)
 RT_HD RT_FI float f32_up_c(double x) {
@@ -1336,6 +1403,8 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       top -= 64;
       return *top;
     };
+    [[maybe_unused]] PlaneOff po{};
+    if constexpr (kFma && RT_SLAB_SIGN) po = plane_offsets(q);
     int cur;
     int lf = 0, ln = 0;
     if (S.root_is_leaf) {
@@ -1403,52 +1472,73 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             cur = pop();
           }
         }
-      } else
-      while (cur >= 0) {
-        if (STATS) cnt.wnode += wave_once();
-        if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them
-        if (STATS) cnt.nodes++;
-        DNode N;
-        if (cur < S.n_lds_nodes) {
-          const RT_LDS DNode &L = lnodes[cur];
+      } else {
+        // the binary walk; LDS_ONLY: every node is staged (a wave-uniform
+        // property of the scene and launch, so the loop is entered in one of
+        // two forms and the per-visit LDS / HBM branch is gone when the whole
+        // tree is in LDS -- C3's persistent instance)
+        auto walk = [&](auto lds_only) {
+          constexpr bool LDS_ONLY = decltype(lds_only)::value;
+          while (cur >= 0) {
+            if (STATS) cnt.wnode += wave_once();
+            if (wave_none(ln == 0)) break; // every walking lane holds a leaf: test them
+            if (STATS) cnt.nodes++;
+            float tn0, tn1;
+            bool h0, h1;
+            int e0, e1;
+            if (kFma && RT_SLAB_SIGN && (LDS_ONLY || cur < S.n_lds_nodes)) {
+              // staged node: sign-selected plane pairs
+              if constexpr (kFma && RT_SLAB_SIGN) slab_hit2_signed(q, po, lnodes + cur, tmin32, cl32, tn0, tn1, h0, h1);
+              e0 = lnodes[cur].entry[0];
+              e1 = lnodes[cur].entry[1];
+            } else {
+              DNode N;
+              if (cur < S.n_lds_nodes) {
+                const RT_LDS DNode &L = lnodes[cur];
 #pragma unroll
-          for (int a = 0; a < 3; ++a)
+                for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              N.lo[a][k] = L.lo[a][k];
-              N.hi[a][k] = L.hi[a][k];
-            }
-          N.entry[0] = L.entry[0];
-          N.entry[1] = L.entry[1];
-        } else {
-          N = S.nodes[cur];
-        }
+                  for (int k = 0; k < 2; ++k) {
+                    N.lo[a][k] = L.lo[a][k];
+                    N.hi[a][k] = L.hi[a][k];
+                  }
+                N.entry[0] = L.entry[0];
+                N.entry[1] = L.entry[1];
+              } else {
+                N = S.nodes[cur];
+              }
 #if RT_SLAB_FMA
-        float tn0, tn1;
-        bool h0, h1;
-        slab_hit2(q, N, tmin32, cl32, tn0, tn1, h0, h1);
+              slab_hit2(q, N, tmin32, cl32, tn0, tn1, h0, h1);
 #else
-        const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
-        const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
-        const float tn0 = slab(q, lo0, hi0, tmin32, cl32);
-        const float tn1 = slab(q, lo1, hi1, tmin32, cl32);
-        const bool h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
+              const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
+              const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
+              tn0 = slab(q, lo0, hi0, tmin32, cl32);
+              tn1 = slab(q, lo1, hi1, tmin32, cl32);
+              h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
 #endif
-        const int e0 = N.entry[0], e1 = N.entry[1];
-        if (h0 && h1) {
-          const bool first0 = tn0 <= tn1;
-          push(first0 ? e1 : e0);
-          cur = first0 ? e0 : e1;
-        } else if (h0 || h1) {
-          cur = h0 ? e0 : e1;
-        } else {
-          cur = pop();
-        }
-        if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
-          lf = (~cur) >> 3;
-          ln = (~cur) & 7;
-          cur = pop();
-        }
+              e0 = N.entry[0];
+              e1 = N.entry[1];
+            }
+            if (h0 && h1) {
+              const bool first0 = tn0 <= tn1;
+              push(first0 ? e1 : e0);
+              cur = first0 ? e0 : e1;
+            } else if (h0 || h1) {
+              cur = h0 ? e0 : e1;
+            } else {
+              cur = pop();
+            }
+            if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
+              lf = (~cur) >> 3;
+              ln = (~cur) & 7;
+              cur = pop();
+            }
+          }
+        };
+        if (kFma && RT_SLAB_SIGN && S.n_lds_nodes >= S.n_nodes)
+          walk(UTag<true>{});
+        else
+          walk(UTag<false>{});
       }
 #if defined(__HIP_DEVICE_COMPILE__)
       if constexpr (kShare) {
