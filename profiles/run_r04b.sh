@@ -1,11 +1,13 @@
 #!/bin/bash
 # r04b: A/B of the sign-selected node planes (build_dbgS0 = RT_SLAB_SIGN=0, the round-3 visit)
-# on C3 and C5, and of the C3 head unit size (RTX_HEAD_STRATA 64 / 128 / 256)
+# on C3 and C5; of the C3 head unit size (RTX_HEAD_STRATA 64 / 128 / 256);
+# and C4's noise cost (build_dbgN: turb() replaced by a constant -- same paths, no Perlin work)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04b
 mkdir -p $O
 bash profiles/ab.sh $O/slab_sign_ab.log "C3" "S0 base" 3 || exit 1
 bash profiles/ab.sh $O/head_strata_ab.log "C3" "RTX_HEAD_STRATA=64 RTX_HEAD_STRATA=128 RTX_HEAD_STRATA=256" 2 || exit 1
+bash profiles/ab.sh $O/noise_cost_ab.log "C4" "base N" 2 || exit 1
 bash profiles/ab.sh $O/slab_sign_ab.log "C5" "S0 base" 1 || exit 1
 echo done

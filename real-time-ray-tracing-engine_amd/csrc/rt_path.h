@@ -993,15 +993,20 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
 #ifndef RT_SLAB_SIGN
 #define RT_SLAB_SIGN 1
 #endif
-struct PlaneOff { // per-ray byte offsets of the near plane pair of each axis in a DNode
+struct PlaneOff { // per-ray byte offsets of the near planes of each axis in a DNode / DNode4
   int n[3];
 };
+// W: children per node (2: DNode, lo[a][*] at 8a, hi at 24 + 8a; 4: DNode4,
+// lo[a][*] at 16a, hi at 48 + 16a); the far planes are at 2 W 4 a + 3 W 4 - n
+template <int W>
 RT_HD RT_FI PlaneOff plane_offsets(const RayF<true> &q) {
   PlaneOff o;
 #pragma unroll
-  for (int a = 0; a < 3; ++a) o.n[a] = 8 * a + (q.inv[a] < 0.0f ? 24 : 0);
+  for (int a = 0; a < 3; ++a) o.n[a] = 4 * W * a + (q.inv[a] < 0.0f ? 12 * W : 0);
   return o;
 }
+template <int W>
+RT_HD RT_FI int far_offset(const PlaneOff &po, int a) { return 8 * W * a + 12 * W - po.n[a]; }
 RT_HD RT_FI float max3f(float a, float b, float c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   float r;
@@ -1027,7 +1032,7 @@ RT_HD RT_FI void slab_hit2_signed(const RayF<true> &q, const PlaneOff &po, const
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const RT_LDS float *pn = (const RT_LDS float *)(b + po.n[a]);
-    const RT_LDS float *pf = (const RT_LDS float *)(b + (16 * a + 24 - po.n[a]));
+    const RT_LDS float *pf = (const RT_LDS float *)(b + far_offset<2>(po, a));
     nr[a][0] = pn[0];
     nr[a][1] = pn[1];
     fr[a][0] = pf[0];
@@ -1046,6 +1051,33 @@ RT_HD RT_FI void slab_hit2_signed(const RayF<true> &q, const PlaneOff &po, const
   t1 = tl[1];
   h0 = tl[0] <= fmaf(th[0], kSlabGrow, q.slack);
   h1 = tl[1] <= fmaf(th[1], kSlabGrow, q.slack);
+}
+// The four children of a staged 4-wide node, planes picked the same way
+// (four floats per 16-B read): entry distance, or +inf for a miss / an empty slot.
+RT_HD RT_FI void slab4_signed(const RayF<true> &q, const PlaneOff &po, const RT_LDS DNode4 *node,
+                              float tmin32, float cl32, float tn[4], int en[4]) {
+  const RT_LDS char *b = (const RT_LDS char *)node;
+  float nr[3][4], fr[3][4];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const RT_LDS float *pn = (const RT_LDS float *)(b + po.n[a]);
+    const RT_LDS float *pf = (const RT_LDS float *)(b + far_offset<4>(po, a));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      nr[a][c] = pn[c];
+      fr[a][c] = pf[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    en[c] = node->entry[c];
+    const float ax = fmaf(nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(fr[0][c], q.inv[0], -q.p[0]);
+    const float ay = fmaf(nr[1][c], q.inv[1], -q.p[1]), by = fmaf(fr[1][c], q.inv[1], -q.p[1]);
+    const float az = fmaf(nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(fr[2][c], q.inv[2], -q.p[2]);
+    const float tl = max3f(ax, ay, fmaxf(az, tmin32));
+    const float th = min3f(bx, by, min3f(bz, cl32, cl32));
+    tn[c] = (en[c] != -1 && tl <= fmaf(th, kSlabGrow, q.slack)) ? tl : __builtin_huge_valf();
+  }
 }
 // f32_up(x) as a canonical float (the min/max operations take it as is
 // instead of re-canonicalising it at every box test)
@@ -1404,7 +1436,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       return *top;
     };
     [[maybe_unused]] PlaneOff po{};
-    if constexpr (kFma && RT_SLAB_SIGN) po = plane_offsets(q);
+    if constexpr (kFma && RT_SLAB_SIGN) po = plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
     int cur;
     int lf = 0, ln = 0;
     if (S.root_is_leaf) {
@@ -1424,29 +1456,33 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           if (STATS) cnt.wnode += wave_once();
           if (wave_none(ln == 0)) break;
           if (STATS) cnt.nodes++;
-          DNode4 N;
-          if (cur < S.n_lds_nodes) {
-            const RT_LDS DNode4 &L = lnodes4[cur];
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-              for (int c = 0; c < 4; ++c) {
-                N.lo[a][c] = L.lo[a][c];
-                N.hi[a][c] = L.hi[a][c];
-              }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) N.entry[c] = L.entry[c];
-          } else {
-            N = nodes4[cur];
-          }
           float tn[4];
           int en[4];
+          if (kFma && RT_SLAB_SIGN && cur < S.n_lds_nodes) { // staged node: sign-selected planes
+            if constexpr (kFma && RT_SLAB_SIGN) slab4_signed(q, po, lnodes4 + cur, tmin32, cl32, tn, en);
+          } else {
+            DNode4 N;
+            if (cur < S.n_lds_nodes) {
+              const RT_LDS DNode4 &L = lnodes4[cur];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float lo[3] = {N.lo[0][c], N.lo[1][c], N.lo[2][c]};
-            const float hi[3] = {N.hi[0][c], N.hi[1][c], N.hi[2][c]};
-            en[c] = N.entry[c];
-            tn[c] = en[c] == -1 ? __builtin_huge_valf() : slab(q, lo, hi, tmin32, cl32);
+              for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                  N.lo[a][c] = L.lo[a][c];
+                  N.hi[a][c] = L.hi[a][c];
+                }
+#pragma unroll
+              for (int c = 0; c < 4; ++c) N.entry[c] = L.entry[c];
+            } else {
+              N = nodes4[cur];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float lo[3] = {N.lo[0][c], N.lo[1][c], N.lo[2][c]};
+              const float hi[3] = {N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+              en[c] = N.entry[c];
+              tn[c] = en[c] == -1 ? __builtin_huge_valf() : slab(q, lo, hi, tmin32, cl32);
+            }
           }
           auto cswap = [&](int x, int y) {
             const bool sw = tn[y] < tn[x];

@@ -1,10 +1,16 @@
 #!/usr/bin/env python3
-"""Per-rank kernel time of an N-way split, measured on ONE GPU (diagnostic).
+"""Per-rank device time of an N-way split, measured on ONE GPU (diagnostic).
 
-For N in 1, 2, 4, 8 renders the share of ranks 0 and N-1 under tile sharding
-(tile t on rank t % N, auto stratum chunks) and stratum sharding, and prints
-the compute-only speedup t(1) / max(t(rank)).  The exchange (gather / reduce)
-is not included.   python tools/shard_sim.py [--config C2]"""
+For N in 1, 2, 4, 8 renders EVERY rank's share under tile sharding (tile t on
+rank t % N, auto stratum chunks -- bench.py's N>1 default) and under stratum
+sharding, each the best of `reps` launches, and adds the library kernels the
+N>1 timed region runs besides the render: each rank's chunk sum
+(rt_tiles_sum_device) and, on rank 0, the tile -> frame reorder
+(rt_tiles_to_frame_device).  Prints the slowest rank's time, the compute-only
+speedup t(1) / max(rank) and the gather payload per rank.  The RCCL gather
+itself (1/N of the frame per rank over xGMI) is not included.
+
+    python tools/shard_sim.py [--config C2] [--reps 3]"""
 import argparse
 import json
 import os
@@ -15,45 +21,68 @@ sys.path.insert(0, os.path.join(ROOT, "real-time-ray-tracing-engine_amd"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 from rtx import abi  # noqa: E402
-from rtx.dist import auto_chunks, tile_counts  # noqa: E402
+from rtx.dist import auto_chunks, device_tiles_sum, device_tiles_to_frame, tile_counts  # noqa: E402
 from rtx.render import Renderer, camera_frame  # noqa: E402
 from rtx.scene import load_scene  # noqa: E402
 from bench import CONFIGS, SCENES  # noqa: E402
 
 
-def best_ms(R, f, reps=3, **kw):
-    ms = []
+def timed(fn, reps):
+    """Best of `reps` device times (ms) of fn() on the current stream."""
+    best = None
     for _ in range(reps):
-        n = kw.pop("_n", None)
-        buf = torch.empty(n, dtype=torch.float64, device="cuda")
-        R.render_device(f, buf.data_ptr(), 0, output=abi.RT_OUT_SUM, accumulate=0, **kw)
-        torch.cuda.synchronize()
-        ms.append(R.last_kernel_ms())
-        kw["_n"] = n
-    return min(ms)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1)
+        best = t if best is None else min(best, t)
+    return best
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     name, width, spp, depth = CONFIGS[a.config]
     S = load_scene(os.path.join(SCENES, name + ".json"))
     f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
     strata = f.sqrt_spp ** 2
+    frame = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda")
     with Renderer(S) as R:
-        t1 = best_ms(R, f, _n=f.image_width * f.image_height * 3)
+        t1 = timed(lambda: R.render_device(f, frame.data_ptr(), 0, output=abi.RT_OUT_SUM,
+                                           accumulate=0), a.reps)
         for N in (1, 2, 4, 8):
             n, t_r = tile_counts(f, N)
             ch = auto_chunks(f, N)
-            tt = max(best_ms(R, f, tiles=(r, N), layout=abi.RT_LAYOUT_TILES, chunks=ch,
-                             _n=t_r * ch * 64 * 3) for r in (0, N - 1))
-            ts = max(best_ms(R, f, samples=(r * strata // N, (r + 1) * strata // N - r * strata // N),
-                             _n=f.image_width * f.image_height * 3) for r in (0, N - 1))
-            print(json.dumps({"config": a.config, "N": N, "t1_ms": round(t1, 3),
-                              "tiles_ms": round(tt, 3), "tiles_chunks": ch,
-                              "tiles_speedup": round(t1 / tt, 2), "strata_ms": round(ts, 3),
-                              "strata_speedup": round(t1 / ts, 2)}), flush=True)
+            buf = torch.empty((t_r, ch, 64, 3), dtype=torch.float64, device="cuda")
+            sums = torch.empty((t_r, 64, 3), dtype=torch.float64, device="cuda")
+            gath = torch.zeros((N, t_r, 64, 3), dtype=torch.float64, device="cuda")
+            per_rank = []
+            for r in range(N):
+                tr = timed(lambda: R.render_device(f, buf.data_ptr(), 0, output=abi.RT_OUT_SUM,
+                                                   accumulate=0, tiles=(r, N),
+                                                   layout=abi.RT_LAYOUT_TILES, chunks=ch), a.reps)
+                ts = timed(lambda: device_tiles_sum(buf, sums), a.reps) if ch > 1 else 0.0
+                per_rank.append(tr + ts)
+            t_frame = timed(lambda: device_tiles_to_frame(gath, f, frame), a.reps)
+            tiles_max = max(per_rank[0] + t_frame, max(per_rank))
+            st = []
+            for r in range(N):
+                b, e = r * strata // N, (r + 1) * strata // N
+                st.append(timed(lambda: R.render_device(f, frame.data_ptr(), 0, samples=(b, e - b),
+                                                        output=abi.RT_OUT_SUM, accumulate=0), a.reps))
+            print(json.dumps({
+                "config": a.config, "N": N, "t1_ms": round(t1, 3), "tiles_chunks": ch,
+                "tiles_rank_ms": [round(x, 3) for x in per_rank],
+                "tiles_chunk_sum_ms": None if ch == 1 else "included per rank",
+                "tiles_reorder_ms_rank0": round(t_frame, 3),
+                "tiles_ms": round(tiles_max, 3), "tiles_speedup": round(t1 / tiles_max, 2),
+                "gather_bytes_per_rank": t_r * 64 * 3 * 8,
+                "strata_rank_ms": [round(x, 3) for x in st], "strata_ms": round(max(st), 3),
+                "strata_speedup": round(t1 / max(st), 2)}), flush=True)
 
 
 if __name__ == "__main__":
