@@ -729,6 +729,13 @@ def main():
         "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
         "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
         "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
+    if st.get("model_trace_max"):
+        # the node-loop SIMD model (STATS): one walk per lane per trip vs each
+        # lane's walks of two consecutive trips back to back (two walks per lane)
+        roof["lane_utilisation"]["traversal_model_one_walk"] = round(
+            st["node_visits"] / (64 * st["model_trace_max"]), 4)
+        roof["lane_utilisation"]["traversal_model_two_walks"] = round(
+            st["node_visits"] / (64 * max(1, st["model_trace_pair_max"])), 4)
     roof["note"] = ("fp64 vector roof (VALU-issue bound, scene LDS/cache resident); "
                     "N>1 lines carry no PMC data (traffic null)"
                     if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")

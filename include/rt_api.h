@@ -282,6 +282,13 @@ typedef struct rt_path_stats {
      pdf, texture evaluation.  Instrumentation adds a few percent; the shares
      are what matters. */
   uint64_t cyc_loop, cyc_regen, cyc_trace, cyc_media, cyc_shade, cyc_lights;
+  /* Traversal-SIMD model (summed over wavefronts): model_trace_max = the sum
+     over path trips of the largest per-lane node-visit count of the trip (the
+     node-loop iterations a wave needs with one walk per lane);
+     model_trace_pair_max = the same with each lane's walks of two consecutive
+     trips run back to back in one node loop (max over lanes of the pair's
+     sum) -- what two walks per lane could at best save. */
+  uint64_t model_trace_max, model_trace_pair_max;
 } rt_path_stats;
 
 typedef struct rt_scene_info {

@@ -10,4 +10,10 @@ bash profiles/ab.sh $O/slab_sign_ab.log "C3" "S0 base" 3 || exit 1
 bash profiles/ab.sh $O/head_strata_ab.log "C3" "RTX_HEAD_STRATA=64 RTX_HEAD_STRATA=128 RTX_HEAD_STRATA=256" 2 || exit 1
 bash profiles/ab.sh $O/noise_cost_ab.log "C4" "base N" 2 || exit 1
 bash profiles/ab.sh $O/slab_sign_ab.log "C5" "S0 base" 1 || exit 1
+for v in S0 base; do
+  if [ $v = base ]; then L=$PWD/real-time-ray-tracing-engine_amd/build/librtx_hip.so; else L=$PWD/real-time-ray-tracing-engine_amd/build_dbg$v/librtx_hip.so; fi
+  echo "== $v" >> $O/arity_sign_ab.log
+  RTX_LIB=$L timeout -k 10 300 python tools/arity_ab.py --n 100000 1000000 --rounds 2 >> $O/arity_sign_ab.log 2>&1 || { tail -20 $O/arity_sign_ab.log; exit 1; }
+done
+tail -12 $O/arity_sign_ab.log
 echo done

@@ -807,6 +807,8 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->cyc_media = h[15];
   stats->cyc_shade = h[16];
   stats->cyc_lights = h[17];
+  stats->model_trace_max = h[18];
+  stats->model_trace_pair_max = h[19];
   return RT_OK;
 }
 

@@ -301,6 +301,15 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   uint64_t cyc_regen = 0;
   const uint64_t t_start = STATS ? clk() : 0;
   uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
+  // traversal-SIMD model (STATS): per trip the largest per-lane visit count,
+  // and for trips paired back to back the largest per-lane sum of the pair
+  uint64_t m_single = 0, m_pair = 0;
+  uint32_t v_prev = 0, m_prev = 0;
+  bool have_prev = false;
+  auto wave_max = [](uint32_t x) {
+    for (int off = 32; off > 0; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off));
+    return x;
+  };
   while (unit < n_units) { // wave-uniform
   const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
   // (wave-uniform) head unit: tile unit / head_chunks; tail unit: a chunk of
@@ -362,10 +371,13 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     if (STATS) cyc_regen += clk() - t_regen; // converged here (every lane)
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
+    uint32_t v_trace = 0;
     if (ps.active) {
       if (STATS) n_segments++;
+      const uint32_t nv0 = cnt.nodes;
       bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
           S, C, ps, key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp);
+      if (STATS) v_trace = cnt.nodes - nv0;
       if (!cont) {
         atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
         atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
@@ -373,6 +385,21 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
         ps.active = false;
       }
     }
+    if (STATS) { // converged: every lane
+      const uint32_t m1 = wave_max(v_trace);
+      m_single += m1;
+      if (!have_prev) {
+        v_prev = v_trace;
+        m_prev = m1;
+      } else {
+        m_pair += wave_max(v_prev + v_trace);
+      }
+      have_prev = !have_prev;
+    }
+  }
+  if (STATS && have_prev) {
+    m_pair += m_prev;
+    have_prev = false;
   }
   __builtin_amdgcn_wave_barrier();
 
@@ -426,7 +453,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
                                         cnt.quads, cnt.other,  cnt.light, cnt.shade,
                                         lane == 0 ? n_trips : 0u, cnt.wnode, cnt.wleaf, cnt.wshade,
                                         lane == 0 ? cyc_loop : 0u, lane == 0 ? cyc_regen : 0u,
-                                        cnt.ctrace, cnt.cmedia, cnt.cshade, cnt.clights};
+                                        cnt.ctrace, cnt.cmedia, cnt.cshade, cnt.clights,
+                                        lane == 0 ? m_single : 0u, lane == 0 ? m_pair : 0u};
     for (int k = 0; k < RT_N_STATS; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);

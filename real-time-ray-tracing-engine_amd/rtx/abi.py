@@ -104,7 +104,8 @@ class PathStats(C.Structure):
         "samples", "segments", "node_visits", "sphere_tests", "quad_tests",
         "other_tests", "light_tests", "shade_events",
         "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters",
-        "cyc_loop", "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights")]
+        "cyc_loop", "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights",
+        "model_trace_max", "model_trace_pair_max")]
 
 
 class SceneInfo(C.Structure):
