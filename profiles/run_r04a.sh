@@ -20,6 +20,8 @@ for c in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_THRE
   if grep -qw "$c" $O/counters.txt; then C="$C $c"; fi
 done
 echo "pmc:$C"
-timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/ubench_pmc -o ub -- real-time-ray-tracing-engine_amd/build/ubench_valu > $O/ubench_pmc.log 2>&1 || { tail -20 $O/ubench_pmc.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ubench_trace -o ub -- real-time-ray-tracing-engine_amd/build/ubench_valu > $O/ubench_trace.log 2>&1 || { tail -20 $O/ubench_trace.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/ubench_pmc -o ub -- real-time-ray-tracing-engine_amd/build/ubench_issue > $O/ubench_pmc.log 2>&1 || { tail -20 $O/ubench_pmc.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ubench_trace -o ub -- real-time-ray-tracing-engine_amd/build/ubench_issue > $O/ubench_trace.log 2>&1 || { tail -20 $O/ubench_trace.log; exit 1; }
+timeout -k 10 60 real-time-ray-tracing-engine_amd/build/ubench_issue > $O/ubench_issue.log 2>&1 || exit 1
+cat $O/ubench_issue.log
 echo done

@@ -1524,9 +1524,11 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             int e0, e1;
             if (kFma && RT_SLAB_SIGN && (LDS_ONLY || cur < S.n_lds_nodes)) {
               // staged node: sign-selected plane pairs
+              // the child entries read first: their LDS latency overlaps the slab math
+              const int2 ee = *(const RT_LDS int2 *)lnodes[cur].entry;
+              e0 = ee.x;
+              e1 = ee.y;
               if constexpr (kFma && RT_SLAB_SIGN) slab_hit2_signed(q, po, lnodes + cur, tmin32, cl32, tn0, tn1, h0, h1);
-              e0 = lnodes[cur].entry[0];
-              e1 = lnodes[cur].entry[1];
             } else {
               DNode N;
               if (cur < S.n_lds_nodes) {
