@@ -81,12 +81,43 @@ def algorithmic_bytes(st, info, n_pixels):
     return b
 
 
-PMC_PASSES = {  # one rocprofv3 --pmc run each (TCC slots: FETCH_SIZE 3, WRITE_SIZE 2 of 4)
-    "valu": ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
-             "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64", "GRBM_GUI_ACTIVE"],
+PMC_PASSES = {  # one rocprofv3 --pmc run each (8 SQ slots; TCC: FETCH_SIZE 3, WRITE_SIZE 2 of 4)
+    "valu": ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_THREAD_CYCLES_VALU",
+             "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+             "SQ_INSTS_VALU_TRANS_F64", "GRBM_GUI_ACTIVE"],
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
 }
+F64_CLASSES = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+               "SQ_INSTS_VALU_TRANS_F64")
+
+
+def valu_figures(c):
+    """The VALU figures of one launch's SQ counters (rocprofv3's gfx950 counter
+    definitions, profiles/r04a_counters_valu.txt; calibrated on saturated
+    instruction streams, profiles/r04a_ubench_*):
+      SQ_ACTIVE_INST_VALU  quad-cycles of VALU issue, one per instruction (four
+                           for a quarter-rate transcendental), summed over SIMDs;
+      SQ_ACTIVE_INST_VALU2 the quad-cycles in which TWO VALU instructions issued
+                           (gfx950 dual-issues: a saturated stream of 32-bit
+                           integer ops issues 1.6, of fp32 FMAs 1.3 instructions
+                           per quad-cycle; fp64 / 3-input ops 0.8-0.9);
+      SQ_THREAD_CYCLES_VALU the same quad-cycles times the active lanes.
+    valu_issue_ratio = ACTIVE / SIMD quad-cycles is rocprofv3's VALUBusy, which
+    exceeds 1 under dual issue; valu_busy = (ACTIVE - ACTIVE2) / SIMD
+    quad-cycles is the share of quad-cycles in which the VALU issues at all
+    (<= 1); valu_lane_fraction = THREAD / (64 ACTIVE) is rocprofv3's
+    VALUUtilization, the mean share of a wave's lanes an issued VALU
+    instruction works for."""
+    simd_quads = c["GRBM_GUI_ACTIVE"] / 8 * 1024 / 4  # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    act = c["SQ_ACTIVE_INST_VALU"]
+    out = {"valu_issue_ratio": round(act / simd_quads, 4)}
+    if "SQ_ACTIVE_INST_VALU2" in c:
+        out["valu_busy"] = round((act - c["SQ_ACTIVE_INST_VALU2"]) / simd_quads, 4)
+        out["valu_dual_issue_share"] = round(c["SQ_ACTIVE_INST_VALU2"] / max(1.0, act), 4)
+    if "SQ_THREAD_CYCLES_VALU" in c:
+        out["valu_lane_fraction"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * max(1.0, act)), 4)
+    return out
 
 
 def pmc_counters(path_glob_root, kernel_tag="render_tiles<false"):
@@ -148,8 +179,8 @@ def pmc_live(args, config=None):
             return None
         res.update(c)
         res["launches_" + name] = n
-    f64 = sum(res[k] for k in PMC_PASSES["valu"][2:6])
-    return {
+    f64 = sum(res[k] for k in F64_CLASSES)
+    return dict(valu_figures(res), **{
         "source": "live: rocprofv3 --pmc passes run by bench.py on this build and workload",
         "hbm_read_bytes_per_launch": int(2 * res["FETCH_SIZE"] * 1024),
         "hbm_write_bytes_per_launch": int(res["WRITE_SIZE"] * 1024),
@@ -158,10 +189,10 @@ def pmc_live(args, config=None):
         "f64_insts_per_launch": int(f64),
         "f64_flops_per_launch": int(64 * (f64 - res["SQ_INSTS_VALU_FMA_F64"])
                                     + 128 * res["SQ_INSTS_VALU_FMA_F64"]),
-        "valu_busy": round(4 * res["SQ_ACTIVE_INST_VALU"] / (res["GRBM_GUI_ACTIVE"] / 8 * 1024), 4),
+        "valu_counters": {k: int(res[k]) for k in PMC_PASSES["valu"]},
         "launches": [res["launches_" + k] for k in PMC_PASSES],
         "config": config,
-    }
+    })
 
 
 def load_pmc(args, config, live):
@@ -195,8 +226,14 @@ def roofline(pmc, kernel_ms):
         tfs = pmc["f64_flops_per_launch"] / kernel_s / 1e12
         roof["achieved"] = round(tfs, 3)
         roof["frac"] = round(tfs / F64_PEAK_TFS, 4)
-    if pmc.get("valu_busy") is not None:
-        roof["valu_busy"] = pmc["valu_busy"]
+    for k in ("valu_busy", "valu_issue_ratio", "valu_dual_issue_share", "valu_lane_fraction"):
+        if pmc.get(k) is not None:
+            roof[k] = pmc[k]
+    if roof["frac"] is not None and pmc.get("valu_lane_fraction") is not None:
+        # fp64 FLOP rate counting only the lanes an instruction works for: the
+        # issued rate x the mean active-lane share of the VALU instructions
+        roof["achieved_active_lanes"] = round(roof["achieved"] * pmc["valu_lane_fraction"], 3)
+        roof["frac_active_lanes"] = round(roof["frac"] * pmc["valu_lane_fraction"], 4)
     if pmc.get("valu_insts_per_launch") and pmc.get("f64_insts_per_launch"):
         roof["f64_inst_share"] = round(pmc["f64_insts_per_launch"] / pmc["valu_insts_per_launch"], 4)
         roof["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]

@@ -58,7 +58,9 @@ def main():
             "f64_insts_per_launch": int(f64),
             "f64_flops_per_launch": int(64 * (f64 - c["SQ_INSTS_VALU_FMA_F64"])
                                         + 128 * c["SQ_INSTS_VALU_FMA_F64"]),
-            "valu_busy": round(4 * c["SQ_ACTIVE_INST_VALU"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4),
+            # rocprofv3's VALUBusy; may exceed 1 (gfx950 dual issue): bench.py
+            # reports valu_busy from SQ_ACTIVE_INST_VALU2 as well (valu_figures)
+            "valu_issue_ratio": round(4 * c["SQ_ACTIVE_INST_VALU"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4),
             "valu_counters": {k: int(v) for k, v in c.items()}})
     print(json.dumps(res, indent=1))
     if a.out:

@@ -6,6 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04b
 mkdir -p $O
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FMA_F32 GRBM_GUI_ACTIVE --output-format csv -d $O/ubench_pmc -o ub -- real-time-ray-tracing-engine_amd/build/ubench_issue > $O/ubench_pmc.log 2>&1 || { tail -20 $O/ubench_pmc.log; exit 1; }
 bash profiles/ab.sh $O/slab_sign_ab.log "C3" "S0 base" 3 || exit 1
 bash profiles/ab.sh $O/head_strata_ab.log "C3" "RTX_HEAD_STRATA=64 RTX_HEAD_STRATA=128 RTX_HEAD_STRATA=256" 2 || exit 1
 bash profiles/ab.sh $O/noise_cost_ab.log "C4" "base N" 2 || exit 1

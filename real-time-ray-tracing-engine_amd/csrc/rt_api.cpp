@@ -586,14 +586,15 @@ int rt_scene_destroy(rt_scene *s) {
 // unit pays a refill drain at its end (its last paths finish while lanes
 // idle) and long units pay it less often.
 //  * Frames of more than 4 tiles per resident wave (1080p: 7.9 on 4,096 wave
-//    slots) with at most RTX_HEAD_STRATA (default 64) strata: whole tiles
-//    written straight into the frame, and the last `slots` x RTX_TAIL_TILES
-//    (default 0.5) tiles in 8 chunks each, the units the waves take last
-//    (dispatch / counter order), so the launch ends on a short unit (C2
-//    +4.5 % over every tile split; profiles/r03e_ab.log).  Head units of
-//    several chunks (more strata) are supported but measured slower than
-//    the uniform split below (C3 -9 % with whole 256-strata tiles, -1.5 %
-//    with a 2-slot tail), and their partials would grow with the strata.
+//    slots) whose head plan keeps the partials within 4 frames: head tiles
+//    whole (up to 64 strata: written straight into the frame, C2) or in
+//    chunks of 128 strata (C3: 2 per tile), and the last `slots` x
+//    RTX_TAIL_TILES (default 0.5) tiles in 8x finer chunks, the units the
+//    waves take last (dispatch / counter order), so the launch ends on a
+//    short unit (C2 +3.9 %, C3 +1.2 % over the uniform split;
+//    profiles/r03f_ab.log).  Whole 256-strata tiles as C3's head: -9 %
+//    (r03e_ab.log, r04b_head_strata_ab.log); chunks of 128 strata measure the
+//    same as 64 with half the partial writes (r04b).
 //  * Otherwise every tile split, ~RTX_CHUNK_TARGET (default 32) units per
 //    wave slot (the round-1 rule), the last tiles again in finer chunks.
 // RTX_CHUNK_TARGET=0: whole tiles only (tests).
@@ -621,7 +622,10 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   };
   double tail = 0.5;
   if (const char *t = std::getenv("RTX_TAIL_TILES")) tail = std::atof(t);
-  int head_max = 64;
+  // head units: whole tiles up to 64 strata (C2); beyond, chunks of 128
+  // strata (C3: 2 per tile -- as fast as 4 chunks of 64, half the partial
+  // writes; whole 256-strata tiles -9 %, profiles/r04b_head_strata_ab.log)
+  int head_max = L.sample_count <= 64 ? 64 : 128;
   if (const char *h = std::getenv("RTX_HEAD_STRATA")) head_max = std::max(1, std::atoi(h));
   const int64_t head_chunks = (L.sample_count + head_max - 1) / head_max;
   int split = 8; // tail chunks per head chunk (RTX_TAIL_SPLIT: A/B runs)

@@ -1025,58 +1025,59 @@ RT_HD RT_FI float min3f(float a, float b, float c) {
   return fminf(fminf(a, b), c);
 #endif
 }
-RT_HD RT_FI void slab_hit2_signed(const RayF<true> &q, const PlaneOff &po, const RT_LDS DNode *node,
-                                  float tmin32, float cl32, float &t0, float &t1, bool &h0, bool &h1) {
-  const RT_LDS char *b = (const RT_LDS char *)node;
-  float nr[3][2], fr[3][2];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const RT_LDS float *pn = (const RT_LDS float *)(b + po.n[a]);
-    const RT_LDS float *pf = (const RT_LDS float *)(b + far_offset<2>(po, a));
-    nr[a][0] = pn[0];
-    nr[a][1] = pn[1];
-    fr[a][0] = pf[0];
-    fr[a][1] = pf[1];
-  }
-  float tl[2], th[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float ax = fmaf(nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(fr[0][c], q.inv[0], -q.p[0]);
-    const float ay = fmaf(nr[1][c], q.inv[1], -q.p[1]), by = fmaf(fr[1][c], q.inv[1], -q.p[1]);
-    const float az = fmaf(nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(fr[2][c], q.inv[2], -q.p[2]);
-    tl[c] = max3f(ax, ay, fmaxf(az, tmin32));
-    th[c] = min3f(bx, by, min3f(bz, cl32, cl32));
-  }
-  t0 = tl[0];
-  t1 = tl[1];
-  h0 = tl[0] <= fmaf(th[0], kSlabGrow, q.slack);
-  h1 = tl[1] <= fmaf(th[1], kSlabGrow, q.slack);
+// One node's sign-picked planes and child entries, read through a byte
+// pointer into the LDS copy (PS = const RT_LDS char *) or into the node table
+// in memory (const char *): a lane's node may be staged or not; the loads
+// differ by address space, the slab math after them is shared, so lanes that
+// diverge on staging repeat only the loads (W = 2: DNode, W = 4: DNode4).
+template <int W>
+struct NodePlanes {
+  float nr[3][W], fr[3][W]; // near / far plane of each axis, per child
+  int en[W];
+};
+template <class T, class PS>
+RT_HD RT_FI T load_at(PS b, int off) { // a T at byte offset off, in b's address space
+  T v;
+  __builtin_memcpy(&v, b + off, sizeof(T));
+  return v;
 }
-// The four children of a staged 4-wide node, planes picked the same way
-// (four floats per 16-B read): entry distance, or +inf for a miss / an empty slot.
-RT_HD RT_FI void slab4_signed(const RayF<true> &q, const PlaneOff &po, const RT_LDS DNode4 *node,
-                              float tmin32, float cl32, float tn[4], int en[4]) {
-  const RT_LDS char *b = (const RT_LDS char *)node;
-  float nr[3][4], fr[3][4];
+// (base: the wave-uniform start of the LDS copy or of the table, node: the
+// lane's node byte offset -- a 32-bit per-lane offset from a scalar base)
+template <int W, class PS>
+RT_HD RT_FI void load_planes(NodePlanes<W> &pl, PS base, int node, const PlaneOff &po) {
+  struct E {
+    int e[W];
+  };
+  struct P {
+    float f[W];
+  };
+  // the child entries first (at 48 in a DNode, 96 in a DNode4): their latency
+  // overlaps the plane reads and the slab math
+  const E e = load_at<E>(base, node + 24 * W);
+#pragma unroll
+  for (int c = 0; c < W; ++c) pl.en[c] = e.e[c];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    const RT_LDS float *pn = (const RT_LDS float *)(b + po.n[a]);
-    const RT_LDS float *pf = (const RT_LDS float *)(b + far_offset<4>(po, a));
+    const P n = load_at<P>(base, node + po.n[a]), f = load_at<P>(base, node + far_offset<W>(po, a));
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      nr[a][c] = pn[c];
-      fr[a][c] = pf[c];
+    for (int c = 0; c < W; ++c) {
+      pl.nr[a][c] = n.f[c];
+      pl.fr[a][c] = f.f[c];
     }
   }
+}
+// The slab verdicts and entry distances of the W children from their planes.
+template <int W>
+RT_HD RT_FI void slab_planes(const RayF<true> &q, const NodePlanes<W> &pl, float tmin32, float cl32,
+                             float tl[W], bool hit[W]) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    en[c] = node->entry[c];
-    const float ax = fmaf(nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(fr[0][c], q.inv[0], -q.p[0]);
-    const float ay = fmaf(nr[1][c], q.inv[1], -q.p[1]), by = fmaf(fr[1][c], q.inv[1], -q.p[1]);
-    const float az = fmaf(nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(fr[2][c], q.inv[2], -q.p[2]);
-    const float tl = max3f(ax, ay, fmaxf(az, tmin32));
+  for (int c = 0; c < W; ++c) {
+    const float ax = fmaf(pl.nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(pl.fr[0][c], q.inv[0], -q.p[0]);
+    const float ay = fmaf(pl.nr[1][c], q.inv[1], -q.p[1]), by = fmaf(pl.fr[1][c], q.inv[1], -q.p[1]);
+    const float az = fmaf(pl.nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(pl.fr[2][c], q.inv[2], -q.p[2]);
+    tl[c] = max3f(ax, ay, fmaxf(az, tmin32));
     const float th = min3f(bx, by, min3f(bz, cl32, cl32));
-    tn[c] = (en[c] != -1 && tl <= fmaf(th, kSlabGrow, q.slack)) ? tl : __builtin_huge_valf();
+    hit[c] = tl[c] <= fmaf(th, kSlabGrow, q.slack);
   }
 }
 // f32_up(x) as a canonical float (the min/max operations take it as is
@@ -1458,8 +1459,19 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           if (STATS) cnt.nodes++;
           float tn[4];
           int en[4];
-          if (kFma && RT_SLAB_SIGN && cur < S.n_lds_nodes) { // staged node: sign-selected planes
-            if constexpr (kFma && RT_SLAB_SIGN) slab4_signed(q, po, lnodes4 + cur, tmin32, cl32, tn, en);
+          if constexpr (kFma && RT_SLAB_SIGN) {
+            NodePlanes<4> pl;
+            if (cur < S.n_lds_nodes)
+              load_planes<4>(pl, (const RT_LDS char *)lnodes4, cur * (int)sizeof(DNode4), po);
+            else
+              load_planes<4>(pl, (const char *)nodes4, cur * (int)sizeof(DNode4), po);
+            bool hh[4];
+            slab_planes<4>(q, pl, tmin32, cl32, tn, hh);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              en[c] = pl.en[c];
+              if (en[c] == -1 || !hh[c]) tn[c] = __builtin_huge_valf();
+            }
           } else {
             DNode4 N;
             if (cur < S.n_lds_nodes) {
@@ -1522,13 +1534,22 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             float tn0, tn1;
             bool h0, h1;
             int e0, e1;
-            if (kFma && RT_SLAB_SIGN && (LDS_ONLY || cur < S.n_lds_nodes)) {
-              // staged node: sign-selected plane pairs
-              // the child entries read first: their LDS latency overlaps the slab math
-              const int2 ee = *(const RT_LDS int2 *)lnodes[cur].entry;
-              e0 = ee.x;
-              e1 = ee.y;
-              if constexpr (kFma && RT_SLAB_SIGN) slab_hit2_signed(q, po, lnodes + cur, tmin32, cl32, tn0, tn1, h0, h1);
+            if constexpr (kFma && RT_SLAB_SIGN) {
+              // sign-picked planes from LDS or from the node table, one slab pass
+              NodePlanes<2> pl;
+              if (LDS_ONLY || cur < S.n_lds_nodes)
+                load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
+              else
+                load_planes<2>(pl, (const char *)S.nodes, cur * (int)sizeof(DNode), po);
+              float tl[2];
+              bool hh[2];
+              slab_planes<2>(q, pl, tmin32, cl32, tl, hh);
+              tn0 = tl[0];
+              tn1 = tl[1];
+              h0 = hh[0];
+              h1 = hh[1];
+              e0 = pl.en[0];
+              e1 = pl.en[1];
             } else {
               DNode N;
               if (cur < S.n_lds_nodes) {

@@ -57,6 +57,29 @@ def test_bench_line_live_pmc():
     assert rf["hbm_frac"] < 1
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["C2", "C3"])
+def test_bench_roofline_counts_issue_and_lanes(config):
+    """The live PMC figures at the headline (C2) and the BVH (C3) configs
+    (VERDICT r3 item 3): valu_busy -- quad-cycles in which the VALU issues at
+    all, (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) over the SIMD quad-cycles
+    -- is <= 1 while rocprofv3's VALUBusy (valu_issue_ratio) may exceed it
+    under gfx950's dual issue; the lane-weighted fp64 fraction (the issued
+    rate x SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU) sits beside frac,
+    below it."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--no-other-configs"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rf = json.loads(r.stdout.strip().splitlines()[-1])["roofline"]
+    assert rf["pmc_source"].startswith("live"), rf.get("pmc_source")
+    assert 0 < rf["valu_busy"] <= 1, rf["valu_busy"]
+    assert rf["valu_issue_ratio"] >= rf["valu_busy"]
+    assert 0 < rf["valu_lane_fraction"] <= 1
+    assert 0 < rf["frac_active_lanes"] <= rf["frac"] <= 1
+    assert rf["frac_active_lanes"] == pytest.approx(rf["frac"] * rf["valu_lane_fraction"], rel=2e-3)
+
+
 def _free_port():
     import socket
     s = socket.socket()

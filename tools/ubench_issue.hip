@@ -45,6 +45,9 @@ __global__ __launch_bounds__(256) void issue(double *sink, int iters) {
       if constexpr (OP == 5) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[c]) : "v"(dc));
       if constexpr (OP == 6) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[c]) : "v"(mb));
       if constexpr (OP == 7) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[c]));
+      // half the lanes active (odd lanes): do the FLOPS / THREAD counters count lanes?
+      if constexpr (OP == 8) if (threadIdx.x & 1) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d[c]) : "v"(db), "v"(dc));
+      if constexpr (OP == 9) if (threadIdx.x & 1) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[c]) : "v"(fb), "v"(fc));
     }
   }
   double s = 0;
@@ -86,5 +89,7 @@ int main() {
   run<5>("v_add_f64", cus);
   run<6>("v_add_u32", cus);
   run<7>("v_rcp_f64", cus);
+  run<8>("v_fma_f64 1/2", cus);
+  run<9>("v_fma_f32 1/2", cus);
   return 0;
 }
