@@ -766,6 +766,9 @@ def main():
         "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
         "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
         "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
+    if st.get("wave_noise_iters"):
+        roof["lane_utilisation"]["noise_albedo"] = round(
+            st["noise_evals"] / (64 * st["wave_noise_iters"]), 4)
     if st.get("model_trace_max"):
         # the node-loop SIMD model (STATS): one walk per lane per trip vs each
         # lane's walks of two consecutive trips back to back (two walks per lane)

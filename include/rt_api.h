@@ -289,6 +289,10 @@ typedef struct rt_path_stats {
      trips run back to back in one node loop (max over lanes of the pair's
      sum) -- what two walks per lane could at best save. */
   uint64_t model_trace_max, model_trace_pair_max;
+  /* Noise-texture albedo evaluations (shading events whose texture is a
+     NoiseTexture): lanes, and wavefront executions of that evaluation (their
+     ratio / 64 is the evaluation's lane use). */
+  uint64_t noise_evals, wave_noise_iters;
 } rt_path_stats;
 
 typedef struct rt_scene_info {

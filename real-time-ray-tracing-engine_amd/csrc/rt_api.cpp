@@ -813,6 +813,8 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->cyc_lights = h[17];
   stats->model_trace_max = h[18];
   stats->model_trace_pair_max = h[19];
+  stats->noise_evals = h[20];
+  stats->wave_noise_iters = h[21];
   return RT_OK;
 }
 

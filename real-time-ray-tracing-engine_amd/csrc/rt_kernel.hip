@@ -297,7 +297,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   int unit = blockIdx.x * BW + wv;
   int *stk = stack_base + wv * S.stack_depth * 64 + lane;
   double *acc = &acc_lds[wv][0][0];
-  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  Counters cnt{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t cyc_regen = 0;
   const uint64_t t_start = STATS ? clk() : 0;
   uint32_t n_samples = 0, n_segments = 0, n_trips = 0;
@@ -454,7 +454,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
                                         lane == 0 ? n_trips : 0u, cnt.wnode, cnt.wleaf, cnt.wshade,
                                         lane == 0 ? cyc_loop : 0u, lane == 0 ? cyc_regen : 0u,
                                         cnt.ctrace, cnt.cmedia, cnt.cshade, cnt.clights,
-                                        lane == 0 ? m_single : 0u, lane == 0 ? m_pair : 0u};
+                                        lane == 0 ? m_single : 0u, lane == 0 ? m_pair : 0u,
+                                        cnt.noise, cnt.wnoise};
     for (int k = 0; k < RT_N_STATS; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);

@@ -26,7 +26,7 @@
 #include <stdint.h>
 
 #define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
-#define RT_N_STATS 20      // counters of the STATS kernel instance (rt_path_stats)
+#define RT_N_STATS 22      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 #define RT_STACK_DEPTH4 64 // 4-wide walks push up to three entries per level
 #ifndef RT_PC_WAVES

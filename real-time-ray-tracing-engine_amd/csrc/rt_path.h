@@ -1118,6 +1118,7 @@ struct Counters {
   uint32_t nodes, spheres, quads, other, light, shade;
   uint32_t wnode, wleaf, wshade; // wave-level iterations (counted by one lane per wave)
   uint64_t ctrace, cmedia, cshade, clights; // wave-level cycles (first active lane adds)
+  uint32_t noise, wnoise; // noise-texture albedo evaluations: lanes, wave executions
 };
 // shader clock for the STATS instance's phase cycles (s_memtime)
 RT_HD RT_FI uint64_t clk() {
@@ -1874,7 +1875,13 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   // albedo: fetched early when a noise texture may run (its long evaluation
   // overlaps less live state there), late otherwise (shorter live range)
   V3 att;
-  if constexpr ((F & F_NOISE) != 0) att = tex_value<F>(S, M.tex, h.p);
+  if constexpr ((F & F_NOISE) != 0) {
+    if (STATS && S.texs[M.tex].kind == RT_TEX_NOISE) {
+      cnt.noise++;
+      cnt.wnoise += wave_once();
+    }
+    att = tex_value<F>(S, M.tex, h.p);
+  }
   V3 w = kMerge ? u1 : unitv(h.n); // ONB(n), ONB.hpp:25-37
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
   V3 ov = unitv(cross(w, a));

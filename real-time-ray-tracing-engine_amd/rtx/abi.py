@@ -105,7 +105,7 @@ class PathStats(C.Structure):
         "other_tests", "light_tests", "shade_events",
         "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters",
         "cyc_loop", "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights",
-        "model_trace_max", "model_trace_pair_max")]
+        "model_trace_max", "model_trace_pair_max", "noise_evals", "wave_noise_iters")]
 
 
 class SceneInfo(C.Structure):
