@@ -1,0 +1,12 @@
+#!/bin/bash
+# r04f: deferred fog albedos, flushed at the trip start (128-point / 96-record pools) -- noise tests,
+# then C4 A/B against build_dbgD0 (immediate noise) and C4 STATS lane use
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04f
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_noise_defer.py -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+bash profiles/ab.sh $O/noise_defer_ab.log "C4" "D0 base" 2 || exit 1
+timeout -k 10 300 python bench.py --config C4 --steps 1 --warmup 1 --no-cpu-baseline --no-other-configs --pmc off > $O/bench_C4_stats.json 2> $O/bench_C4_stats.err || { tail -20 $O/bench_C4_stats.err; exit 1; }
+echo done

@@ -980,8 +980,10 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
   h0 = slab_hit(q, lo0, hi0, tmin32, cl32, t0);
   h1 = slab_hit(q, lo1, hi1, tmin32, cl32, t1);
 }
-// Both children of a binary node staged in LDS, with the planes picked by the
-// ray's direction signs (RT_SLAB_SIGN): for an axis with 1/d >= 0 the lo plane
+// Node planes picked by the ray's direction signs (RT_SLAB_SIGN) -- the
+// binary walk over a fully staged tree (C3: +8 %, C5: +8 %, profiles/
+// r04b_slab_sign_ab.log) and every 4-wide visit (100k / 1M spheres +10 %,
+// r04c_arity_sign_ab.log): for an axis with 1/d >= 0 the lo plane
 // gives the entry distance and the hi plane the exit, the other way round for
 // 1/d < 0 -- fma(plane, 1/d, -P) is monotone in the plane for a fixed 1/d, and
 // every operand is finite (1/d and P are clamped, ray_f32), so min / max of
@@ -1535,13 +1537,14 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             float tn0, tn1;
             bool h0, h1;
             int e0, e1;
-            if constexpr (kFma && RT_SLAB_SIGN) {
-              // sign-picked planes from LDS or from the node table, one slab pass
+            if constexpr (kFma && RT_SLAB_SIGN && LDS_ONLY) {
+              // the whole tree staged: sign-picked planes from LDS.  (From the
+              // node table in memory the six 8-B loads instead of four 16-B
+              // ones lost 14-17 % on 100k-1M spheres, and a per-lane choice
+              // between the two forms runs both slab passes in a mixed wave:
+              // -6.5 %, profiles/r04b_arity_sign_ab.log, r04c_arity_sign_ab.log.)
               NodePlanes<2> pl;
-              if (LDS_ONLY || cur < S.n_lds_nodes)
-                load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
-              else
-                load_planes<2>(pl, (const char *)S.nodes, cur * (int)sizeof(DNode), po);
+              load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
               float tl[2];
               bool hh[2];
               slab_planes<2>(q, pl, tmin32, cl32, tl, hh);
