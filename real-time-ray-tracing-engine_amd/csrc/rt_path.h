@@ -1068,6 +1068,26 @@ RT_HD RT_FI void load_planes(NodePlanes<W> &pl, PS base, int node, const PlaneOf
     }
   }
 }
+// Both children of a binary node from their picked planes, verdicts returned
+// as two bools (an array of them made the compiler build the visit's branch
+// masks with VALU selects: C3 -1.6 %, profiles/r04g_c3_build_ab.log)
+RT_HD RT_FI void slab2_planes(const RayF<true> &q, const NodePlanes<2> &pl, float tmin32, float cl32,
+                              float &t0, float &t1, bool &h0, bool &h1) {
+  float th[2];
+  float tl[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float ax = fmaf(pl.nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(pl.fr[0][c], q.inv[0], -q.p[0]);
+    const float ay = fmaf(pl.nr[1][c], q.inv[1], -q.p[1]), by = fmaf(pl.fr[1][c], q.inv[1], -q.p[1]);
+    const float az = fmaf(pl.nr[2][c], q.inv[2], -q.p[2]), bz = fmaf(pl.fr[2][c], q.inv[2], -q.p[2]);
+    tl[c] = max3f(ax, ay, fmaxf(az, tmin32));
+    th[c] = min3f(bx, by, min3f(bz, cl32, cl32));
+  }
+  t0 = tl[0];
+  t1 = tl[1];
+  h0 = tl[0] <= fmaf(th[0], kSlabGrow, q.slack);
+  h1 = tl[1] <= fmaf(th[1], kSlabGrow, q.slack);
+}
 // The slab verdicts and entry distances of the W children from their planes.
 template <int W>
 RT_HD RT_FI void slab_planes(const RayF<true> &q, const NodePlanes<W> &pl, float tmin32, float cl32,
@@ -1545,13 +1565,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
               // -6.5 %, profiles/r04b_arity_sign_ab.log, r04c_arity_sign_ab.log.)
               NodePlanes<2> pl;
               load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
-              float tl[2];
-              bool hh[2];
-              slab_planes<2>(q, pl, tmin32, cl32, tl, hh);
-              tn0 = tl[0];
-              tn1 = tl[1];
-              h0 = hh[0];
-              h1 = hh[1];
+              slab2_planes(q, pl, tmin32, cl32, tn0, tn1, h0, h1);
               e0 = pl.en[0];
               e1 = pl.en[1];
             } else {
