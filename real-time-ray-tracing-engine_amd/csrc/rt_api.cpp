@@ -546,8 +546,6 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.quad_bytes = (int32_t)sizeof(DQuad);
   in.device_bytes = (int64_t)off;
   in.features = d.features;
-  // after every plan and table lookup keyed by the instance features: not a key
-  if (H.sphere_items && !H.device_bvh && RT_SPHERE_ITEMS) d.features |= RT_FEAT_SPHERE_ITEMS;
   in.lds_nodes = d.n_lds_nodes;
   in.bvh_builder = builder;
   in.bvh_arity = H.bvh_arity;

@@ -185,13 +185,6 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_NOISE 8  // Perlin noise textures
 #define RT_FEAT_FLAT 16  // flat world (root_is_leaf): no BVH walk
 #define RT_FEAT_BVH4 32  // the world BVH is 4-wide (DNode4); never with RT_FEAT_FLAT
-// not an instance key (outside F_ALL): world item i is sphere i with no
-// transform chain (rt_scene.cpp orders the spheres so), so a leaf test reads the
-// sphere without the item record first
-#define RT_FEAT_SPHERE_ITEMS 64
-#ifndef RT_SPHERE_ITEMS
-#define RT_SPHERE_ITEMS 1 // 0: never set (A/B)
-#endif
 
 // LDS plan of one render instance (rtk_lds_plan): its occupancy target and
 // what the per-block LDS share at that occupancy leaves for staged BVH nodes.

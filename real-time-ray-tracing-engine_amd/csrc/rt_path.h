@@ -995,11 +995,6 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
 #ifndef RT_SLAB_SIGN
 #define RT_SLAB_SIGN 1
 #endif
-// RT_PARK2: a lane that meets a second leaf while one is parked parks that one
-// too (pk) and keeps walking; it leaves the node loop at its third leaf
-#ifndef RT_PARK2
-#define RT_PARK2 0
-#endif
 struct PlaneOff { // per-ray byte offsets of the near planes of each axis in a DNode / DNode4
   int n[3];
 };
@@ -1309,12 +1304,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   auto item_root_t = [&](auto uniform, int ii, const Ray &rr, double ra, double ry, double tmax,
                          double &t) -> bool {
     constexpr bool U = decltype(uniform)::value && RT_UNIFORM_LOADS_F(F);
-    if constexpr (!kFlat && (F & F_XFORM) == 0 && RT_SPHERE_ITEMS) {
-      if (S.features & RT_FEAT_SPHERE_ITEMS) { // item ii is sphere ii: no item record
-        if (STATS) cnt.spheres++;
-        return sphere_root(load_sphere<LP>(S, lp, ii), rr, ra, tmin, tmax, t, moving, true, ry);
-      }
-    }
     const DItem it = U ? ldu<U>(S.items, ii) : load_item<LP>(S, lp, ii);
     Ray lr = rr;
     double al = ra;
@@ -1474,7 +1463,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     if constexpr (kFma && RT_SLAB_SIGN) po = plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
     int cur;
     int lf = 0, ln = 0;
-    [[maybe_unused]] int pk = 0; // RT_PARK2: a second parked leaf (its entry), 0 none
     if (S.root_is_leaf) {
       cur = -1;
       ln = S.n_root_items;
@@ -1554,12 +1542,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             ln = (~cur) & 7;
             cur = pop();
           }
-#if RT_PARK2
-          if (!kShare && cur < -1 && pk == 0) { // second leaf: park it as well
-            pk = cur;
-            cur = pop();
-          }
-#endif
         }
       } else {
         // the binary walk; LDS_ONLY: every node is staged (a wave-uniform
@@ -1628,12 +1610,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
               ln = (~cur) & 7;
               cur = pop();
             }
-#if RT_PARK2
-            if (!kShare && cur < -1 && pk == 0) { // second leaf: park it as well
-              pk = cur;
-              cur = pop();
-            }
-#endif
           }
         };
         if (kFma && RT_SLAB_SIGN && S.n_lds_nodes >= S.n_nodes)
@@ -1676,33 +1652,9 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           ++lf;
           --ln;
           test_item(UTag<false>{}, ii);
-#if RT_PARK2 == 1
-          if (ln == 0 && pk != 0) { // then the second parked leaf
-            lf = (~pk) >> 3;
-            ln = (~pk) & 7;
-            pk = 0;
-          }
-#endif
         }
-#if RT_PARK2 == 2
-        // one leaf per lane per leaf phase: the second parked leaf moves up
-        if (ln == 0 && pk != 0) {
-          lf = (~pk) >> 3;
-          ln = (~pk) & 7;
-          pk = 0;
-        }
-        if (cur < -1 && ln == 0) {
-          lf = (~cur) >> 3;
-          ln = (~cur) & 7;
-          cur = pop();
-        }
-        if (cur < -1 && pk == 0) {
-          pk = cur;
-          cur = pop();
-        }
-#endif
       }
-      if (cur < -1 && ln == 0) { // a second leaf met while one was parked: it is next
+      if (cur < -1) { // a second leaf met while one was parked: it is next
         lf = (~cur) >> 3;
         ln = (~cur) & 7;
         cur = pop();

@@ -959,36 +959,7 @@ struct Compiler {
     } else {
       SahBuilder(H).emit_world_bvh(ibox);
     }
-    if (!emit_lights()) return false;
-    if (!device) spheres_in_item_order();
-    return true;
-  }
-
-  // Store the spheres in the world items' (leaf) order when every world item is
-  // a distinct sphere without a transform chain and there are no media: then
-  // items[i].idx == i and the kernel's leaf test reads sphere i directly
-  // (RT_FEAT_SPHERE_ITEMS).  Spheres only lights use follow; the light records
-  // are remapped.  The order of the sphere table changes no result.
-  void spheres_in_item_order() {
-    if (H.items.empty() || !H.bitems.empty() || !H.mitems.empty()) return;
-    std::vector<int> new_of(H.spheres.size(), -1);
-    for (size_t i = 0; i < H.items.size(); ++i) {
-      const DItem &it = H.items[i];
-      if (it.kind != I_SPHERE || it.xf_count != 0 || it.idx < 0 ||
-          it.idx >= (int)H.spheres.size() || new_of[it.idx] >= 0)
-        return;
-      new_of[it.idx] = (int)i;
-    }
-    int next = (int)H.items.size();
-    for (int &n : new_of)
-      if (n < 0) n = next++;
-    std::vector<DSphere> sp(H.spheres.size());
-    for (size_t k = 0; k < H.spheres.size(); ++k) sp[new_of[k]] = H.spheres[k];
-    H.spheres.swap(sp);
-    for (DItem &it : H.items) it.idx = new_of[it.idx];
-    for (DLight &L : H.lights)
-      if (L.kind == I_SPHERE) L.idx = new_of[L.idx];
-    H.sphere_items = 1;
+    return emit_lights();
   }
 };
 

@@ -34,9 +34,6 @@ struct HostScene {
   // in scene order, their boxes (lo xyz, hi xyz) and the centroid bounds; nodes
   // sized, not filled
   int32_t device_bvh = 0;
-  // 1: every world item is a sphere without transforms and items[i].idx == i
-  // (the spheres stored in the items' leaf order; DScene RT_FEAT_SPHERE_ITEMS)
-  int32_t sphere_items = 0;
   std::vector<double> item_boxes;
   double scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
 };
