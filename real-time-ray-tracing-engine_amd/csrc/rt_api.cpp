@@ -507,7 +507,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       rt_scene_destroy(s);
       return set_err(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(be));
     }
-    const int64_t node_b = (d.features & RT_FEAT_BVH4) ? (int64_t)sizeof(DNode4) : (int64_t)sizeof(DNode);
+    const int64_t node_b = RT_LDS_NODE_BYTES(d.features);
     d.n_lds_nodes_pc = pc_free < 0 ? -1 : (int32_t)std::min<int64_t>(pc_free / node_b, d.n_nodes);
     if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) // A/B experiments
       if (d.n_lds_nodes_pc >= 0) // within what the plan leaves free

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   int *stack_base = reinterpret_cast<int *>(dyn_lds);
   DNode *lnodes_g = reinterpret_cast<DNode *>(stack_base + BW * S.stack_depth * 64);
   const RT_LDS DNode *lnodes = (const RT_LDS DNode *)lnodes_g; // DNode4 in BVH4 instances
-  constexpr int kNodeBytes = (F & F_BVH4) ? (int)sizeof(DNode4) : (int)sizeof(DNode);
+  constexpr int kNodeBytes = RT_LDS_NODE_BYTES(F);
   // persistent instance: world items and spheres after the nodes (LdsPrims)
   LdsPrims lp{nullptr, nullptr};
   int4 *prim_g = reinterpret_cast<int4 *>(lnodes_g) + (size_t)max(0, S.n_lds_nodes) * (kNodeBytes / 16);
@@ -263,10 +263,32 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
   }
   if (S.n_lds_nodes > 0 || (PC && S.lds_items_pc > 0)) { // stage once per block
-    const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
-    int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
-    const int n16 = max(0, S.n_lds_nodes) * (kNodeBytes / 16);
-    for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    if constexpr ((F & F_BVH4) != 0 || !RT_LDS_TRIPLE) {
+      const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
+      int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
+      const int n16 = max(0, S.n_lds_nodes) * (kNodeBytes / 16);
+      for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    } else {
+      // binary nodes as DNodeL: 8-B unit j of staged node i is, per axis a =
+      // j / 3, the lo pair (8a in the DNode), the hi pair (24 + 8a), the lo pair
+      // again; unit 9 the child entries (48) -- inner children as DNodeL byte
+      // offsets when the whole tree is staged (the LDS-only walk's `cur`)
+      const uint2 *src = reinterpret_cast<const uint2 *>(S.nodes);
+      uint2 *dst = reinterpret_cast<uint2 *>(lnodes_g);
+      const int n8 = max(0, S.n_lds_nodes) * 10;
+      const bool whole = RT_SLAB_FMA && RT_SLAB_SIGN && S.n_lds_nodes >= S.n_nodes; // trace()'s LDS-only walk
+      for (int k = threadIdx.x; k < n8; k += blockDim.x) {
+        const int i = k / 10, j = k - 10 * (k / 10);
+        const int a = j / 3, m = j - 3 * (j / 3);
+        const int u = j == 9 ? 6 : (m == 1 ? 3 + a : a);
+        uint2 v = src[8 * i + u];
+        if (j == 9 && whole) {
+          if ((int)v.x >= 0) v.x *= (unsigned)sizeof(DNodeL);
+          if ((int)v.y >= 0) v.y *= (unsigned)sizeof(DNodeL);
+        }
+        dst[k] = v;
+      }
+    }
     if constexpr (PC) {
       if (S.lds_items_pc > 0) {
         const int ni = S.lds_items_pc * 2, ns = S.lds_spheres_pc * 4; // int4 per DItem / DSphere
@@ -588,13 +610,13 @@ const RenderFn *render_table(bool stats) {
 
 // ---------------------------------------------------------------- launchers
 extern "C" size_t rtk_lds_bytes(int features, int stack_depth, int n_lds_nodes) {
-  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  const size_t node = RT_LDS_NODE_BYTES(features);
   return (size_t)block_waves((unsigned)features) * stack_depth * 64 * sizeof(int) +
          (size_t)n_lds_nodes * node;
 }
 // a persistent instance's dynamic LDS (pcw waves per block)
 static size_t lds_bytes_pc(int features, int pcw, int stack_depth, int n_lds_nodes) {
-  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  const size_t node = RT_LDS_NODE_BYTES(features);
   return (size_t)pcw * stack_depth * 64 * sizeof(int) + (size_t)n_lds_nodes * node;
 }
 
@@ -619,7 +641,7 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   size_t per_block = lds_cu / blocks_per_cu;
   if (per_block > cap) per_block = cap;
   const size_t fixed = a.sharedSizeBytes + rtk_lds_bytes(features, stack_depth, 0);
-  const size_t node = (features & F_BVH4) ? sizeof(DNode4) : sizeof(DNode);
+  const size_t node = RT_LDS_NODE_BYTES(features);
   plan->waves_per_simd = waves_per_simd;
   plan->block_budget = (int32_t)per_block;
   plan->fixed_bytes = (int32_t)fixed;

@@ -96,6 +96,33 @@ struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + li
 };
 static_assert(sizeof(DNode) == 64, "DNode layout");
 
+// A binary node as the kernels stage it in LDS (80 B): per axis the children's
+// lo planes, hi planes and lo planes again, so that a ray's near and far plane
+// pairs (sign-picked: near = lo for 1/d_a >= 0, hi otherwise) are adjacent for
+// either sign -- one 16-B read per axis at byte 24 a + 8 s_a instead of two
+// 8-B reads at unrelated offsets (rt_path.h load_planes_l).  RT_LDS_TRIPLE 0:
+// nodes are staged as DNode (A/B).
+#ifndef RT_LDS_TRIPLE
+#define RT_LDS_TRIPLE 1
+#endif
+struct DNodeL {
+  float p[3][3][2]; // p[axis][0] = lo[axis][*], p[axis][1] = hi[axis][*], p[axis][2] = lo[axis][*]
+  int32_t entry[2];
+};
+static_assert(sizeof(DNodeL) == 80, "DNodeL layout");
+// (whole: the whole tree is staged -- inner children as DNodeL byte offsets)
+inline DNodeL lds_node(const DNode &n, bool whole) {
+  DNodeL l;
+  for (int a = 0; a < 3; ++a)
+    for (int k = 0; k < 2; ++k) {
+      l.p[a][0][k] = l.p[a][2][k] = n.lo[a][k];
+      l.p[a][1][k] = n.hi[a][k];
+    }
+  for (int k = 0; k < 2; ++k)
+    l.entry[k] = whole && n.entry[k] >= 0 ? n.entry[k] * (int32_t)sizeof(DNodeL) : n.entry[k];
+  return l;
+}
+
 // 4-wide BVH node (128 B): the boxes of up to four children in SoA order
 // (lo x[4], lo y[4], lo z[4], hi x[4], ...), fp32 rounded outward like DNode's,
 // and their entries with DNode's encoding (-1 = empty slot).  Collapsed from the
@@ -185,6 +212,9 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_NOISE 8  // Perlin noise textures
 #define RT_FEAT_FLAT 16  // flat world (root_is_leaf): no BVH walk
 #define RT_FEAT_BVH4 32  // the world BVH is 4-wide (DNode4); never with RT_FEAT_FLAT
+// bytes per BVH node staged in LDS (DNode4 / DNodeL / DNode)
+#define RT_LDS_NODE_BYTES(features)                                                                \
+  (((features) & RT_FEAT_BVH4) ? (int)sizeof(DNode4) : RT_LDS_TRIPLE ? (int)sizeof(DNodeL) : (int)sizeof(DNode))
 
 // LDS plan of one render instance (rtk_lds_plan): its occupancy target and
 // what the per-block LDS share at that occupancy leaves for staged BVH nodes.

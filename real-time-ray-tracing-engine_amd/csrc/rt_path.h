@@ -1007,6 +1007,14 @@ RT_HD RT_FI PlaneOff plane_offsets(const RayF<true> &q) {
   for (int a = 0; a < 3; ++a) o.n[a] = 4 * W * a + (q.inv[a] < 0.0f ? 12 * W : 0);
   return o;
 }
+// in a DNodeL (binary nodes staged in LDS, RT_LDS_TRIPLE): the near pair at
+// 24 a + 8 s_a, the far pair 8 B after it
+RT_HD RT_FI PlaneOff plane_offsets_l(const RayF<true> &q) {
+  PlaneOff o;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) o.n[a] = 24 * a + (q.inv[a] < 0.0f ? 8 : 0);
+  return o;
+}
 template <int W>
 RT_HD RT_FI int far_offset(const PlaneOff &po, int a) { return 8 * W * a + 12 * W - po.n[a]; }
 RT_HD RT_FI float max3f(float a, float b, float c) {
@@ -1065,6 +1073,37 @@ RT_HD RT_FI void load_planes(NodePlanes<W> &pl, PS base, int node, const PlaneOf
     for (int c = 0; c < W; ++c) {
       pl.nr[a][c] = n.f[c];
       pl.fr[a][c] = f.f[c];
+    }
+  }
+}
+// The same from a DNodeL in LDS: per axis the near and far pairs as one 16-B
+// read (ds_read2_b64), the entries at 72
+template <class PS>
+RT_HD RT_FI void load_planes_l(NodePlanes<2> &pl, PS base, int node, const PlaneOff &po) {
+  struct E {
+    int e[2];
+  };
+  struct P {
+    float n[2], f[2];
+  };
+#if defined(__HIP_DEVICE_COMPILE__)
+  // DNodeL offsets are multiples of 80, the pair offsets of 8: each axis read
+  // is an 8-B aligned ds_read2_b64 (not an unaligned ds_read_b128)
+  __builtin_assume((node & 15) == 0);
+#endif
+  const E e = load_at<E>(base, node + 72);
+  pl.en[0] = e.e[0];
+  pl.en[1] = e.e[1];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_assume((po.n[a] & 7) == 0);
+#endif
+    const P v = load_at<P>(base, node + po.n[a]);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      pl.nr[a][c] = v.n[c];
+      pl.fr[a][c] = v.f[c];
     }
   }
 }
@@ -1272,8 +1311,9 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
 
 // Closest hit over the world BVH.  Primitive items record only (t, item) during
 // traversal and build the hit record once at the end; media build theirs when hit.
-// `lnodes` is the LDS copy of nodes [0, S.n_lds_nodes) (the host emulator passes
-// S.nodes itself).
+// `lnodes` is the LDS copy of nodes [0, S.n_lds_nodes): DNode4 for 4-wide trees,
+// DNodeL for binary ones (RT_LDS_TRIPLE; the host emulator passes the same forms
+// of the whole tree).
 template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                                       uint32_t bounce, int *stk, const RT_LDS DNode *lnodes,
@@ -1460,7 +1500,8 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       return *top;
     };
     [[maybe_unused]] PlaneOff po{};
-    if constexpr (kFma && RT_SLAB_SIGN) po = plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
+    if constexpr (kFma && RT_SLAB_SIGN)
+      po = ((F & F_BVH4) == 0 && RT_LDS_TRIPLE) ? plane_offsets_l(q) : plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
     int cur;
     int lf = 0, ln = 0;
     if (S.root_is_leaf) {
@@ -1564,13 +1605,26 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
               // between the two forms runs both slab passes in a mixed wave:
               // -6.5 %, profiles/r04b_arity_sign_ab.log, r04c_arity_sign_ab.log.)
               NodePlanes<2> pl;
-              load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
+              if constexpr (RT_LDS_TRIPLE) // cur: the node's byte offset (entries staged so)
+                load_planes_l(pl, (const RT_LDS char *)lnodes, cur, po);
+              else
+                load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
               slab2_planes(q, pl, tmin32, cl32, tn0, tn1, h0, h1);
               e0 = pl.en[0];
               e1 = pl.en[1];
             } else {
               DNode N;
               if (cur < S.n_lds_nodes) {
+#if RT_LDS_TRIPLE
+                const RT_LDS DNodeL &L = ((const RT_LDS DNodeL *)lnodes)[cur];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                  for (int k = 0; k < 2; ++k) {
+                    N.lo[a][k] = L.p[a][0][k];
+                    N.hi[a][k] = L.p[a][1][k];
+                  }
+#else
                 const RT_LDS DNode &L = lnodes[cur];
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
@@ -1579,6 +1633,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                     N.lo[a][k] = L.lo[a][k];
                     N.hi[a][k] = L.hi[a][k];
                   }
+#endif
                 N.entry[0] = L.entry[0];
                 N.entry[1] = L.entry[1];
               } else {

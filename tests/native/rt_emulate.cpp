@@ -23,7 +23,7 @@ namespace {
 
 template <unsigned F>
 void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, int i, int j,
-                 int s0, int s1, int *stk, double acc[3]) {
+                 int s0, int s1, int *stk, const DNode *ln, double acc[3]) {
   Counters cnt{};
   for (int k = s0; k < s1; ++k) {
     Key key{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)(j * C.W + i), (uint32_t)k};
@@ -33,7 +33,7 @@ void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, i
     ps.bounce = 0;
     ps.active = C.max_depth > 0;
     while (ps.active) {
-      bool cont = segment<false, F>(S, C, ps, key, stk, S.nodes, cnt);
+      bool cont = segment<false, F>(S, C, ps, key, stk, ln, cnt);
       if (!cont) {
         acc[0] += ps.T.x;
         acc[1] += ps.T.y;
@@ -45,7 +45,7 @@ void trace_pixel(const DScene &S, const DCamera &C, const rt_render_params &p, i
 }
 
 typedef void (*PixelFn)(const DScene &, const DCamera &, const rt_render_params &, int, int, int,
-                        int, int *, double *);
+                        int, int *, const DNode *, double *);
 template <unsigned... Fs>
 constexpr std::array<PixelFn, sizeof...(Fs)> pixel_fns(std::integer_sequence<unsigned, Fs...>) {
   return {trace_pixel<Fs>...};
@@ -89,7 +89,14 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   S.static_spheres = rtx::all_spheres_static(H);
   S.stack_depth = bvh4 ? rtx::bvh4_stack_depth(depth4)
                        : std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
-  S.n_lds_nodes = S.n_nodes; // host: the "LDS" copy is the array itself
+  S.n_lds_nodes = S.n_nodes; // host: the whole tree is the "LDS" copy
+  // in the form the kernel stages it: DNode4 as is, binary nodes as DNodeL
+  std::vector<DNodeL> lnodes_l;
+  const DNode *ln = S.nodes;
+  if (!bvh4 && RT_LDS_TRIPLE) {
+    for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, RT_SLAB_FMA && RT_SLAB_SIGN));
+    ln = (const DNode *)(const void *)lnodes_l.data();
+  }
   DCamera C;
   auto cp = [](double *d, const rt_vec3 &v) {
     d[0] = v.x;
@@ -121,7 +128,7 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   for (int j = r0; j < r1; ++j)
     for (int i = 0; i < C.W; ++i) {
       double acc[3] = {0, 0, 0};
-      fn(S, C, *p, i, j, s0, s1, stack.data(), acc);
+      fn(S, C, *p, i, j, s0, s1, stack.data(), ln, acc);
       double sc = (p->output == RT_OUT_SCALED) ? C.scale : 1.0;
       double *o = out + 3 * ((size_t)(j - r0) * C.W + i);
       o[0] = (p->output == RT_OUT_SCALED) ? sc * acc[0] : acc[0];
