@@ -282,10 +282,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
         const int a = j / 3, m = j - 3 * (j / 3);
         const int u = j == 9 ? 6 : (m == 1 ? 3 + a : a);
         uint2 v = src[8 * i + u];
-        if (j == 9 && whole) { // RT_LDS_ABS: as LDS byte addresses
-          const unsigned b = RT_LDS_ABS ? (unsigned)(uintptr_t)lnodes : 0u;
-          if ((int)v.x >= 0) v.x = b + v.x * (unsigned)sizeof(DNodeL);
-          if ((int)v.y >= 0) v.y = b + v.y * (unsigned)sizeof(DNodeL);
+        if (j == 9 && whole) {
+          if ((int)v.x >= 0) v.x *= (unsigned)sizeof(DNodeL);
+          if ((int)v.y >= 0) v.y *= (unsigned)sizeof(DNodeL);
         }
         dst[k] = v;
       }

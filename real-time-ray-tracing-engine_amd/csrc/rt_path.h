@@ -79,19 +79,6 @@ RT_HD RT_FI double sqrt_n(double x) {
   return sqrt(x);
 #endif
 }
-// Correctly rounded sqrt of a discriminant (any x >= 0): sqrt_n unless a lane
-// of the wave has 0 < x < 2^-767 (a grazing ray), then the full lowering for
-// the whole wave -- a uniform branch on one compare instead of the input and
-// output scaling in every sphere test.
-#ifndef RT_SQRT_D
-#define RT_SQRT_D 1
-#endif
-RT_HD RT_FI double sqrt_d(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SQRT_N && RT_SQRT_D
-  if (__builtin_expect(__ballot(x < 0x1p-767 && x != 0.0) == 0, 1)) return sqrt_n(x);
-#endif
-  return sqrt(x);
-}
 // Correctly rounded 1/x for x in [2^-600, 2^600] or +inf: the compiler's fp64
 // division lowering with numerator 1 (v_rcp_f64, two Newton steps, one
 // Markstein correction) without v_div_scale (a no-op in that range) and with a
@@ -549,7 +536,7 @@ RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tm
   double c = len2(oc) - s.rr;
   double disc = h * h - a * c;
   if (disc < 0) return false;
-  double sq = sqrt_d(disc);
+  double sq = sqrt(disc);
   // mk: ya = RN(1/a) shared by every root of one ray (div_mk), else the division
   double t = (RT_MK_SPHERE && mk) ? div_mk(h - sq, a, ya) : (h - sq) / a;
   if (!(tmin < t && t < tmax)) {
@@ -755,7 +742,7 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
       double cc2 = len2(oc) - sp.rr;
       double disc = h * h - a * cc2;
       if (disc < 0) continue;
-      double sq = sqrt_d(disc);
+      double sq = sqrt(disc);
       double r1 = (h - sq) / a, r2 = (h + sq) / a;
       if (-kInf < r1 && r1 < kInf) keep(r1, 0u);
       if (-kInf < r2 && r2 < kInf) keep(r2, 0u);
@@ -814,7 +801,7 @@ RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin
   if (t2 > tmax) t2 = tmax;
   if (t1 >= t2) return false;
   if (t1 < 0) t1 = 0;
-  double rl = sqrt_d(len2(r.d));
+  double rl = sqrt(len2(r.d));
   double inside = (t2 - t1) * rl;
   double uu[4];
   u01x4(key, bounce, kSlotMediumBase + (uint32_t)M.id, uu);
@@ -1008,15 +995,6 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
 #ifndef RT_SLAB_SIGN
 #define RT_SLAB_SIGN 1
 #endif
-// RT_LDS_ABS: the staged child entries of a wholly staged binary tree are LDS
-// byte addresses, so the visit adds no base (device only; 0: offsets, A/B)
-#ifndef RT_LDS_ABS
-#define RT_LDS_ABS 1
-#endif
-// RT_VISIT_SELECT: the binary visit's push / advance / pop as selects (A/B)
-#ifndef RT_VISIT_SELECT
-#define RT_VISIT_SELECT 0
-#endif
 struct PlaneOff { // per-ray byte offsets of the near planes of each axis in a DNode / DNode4
   int n[3];
 };
@@ -1109,11 +1087,10 @@ RT_HD RT_FI void load_planes_l(NodePlanes<2> &pl, PS base, int node, const Plane
     float n[2], f[2];
   };
 #if defined(__HIP_DEVICE_COMPILE__)
-  // DNodeL offsets are multiples of 80 from a 16-B aligned copy, the pair
+  // DNodeL offsets are multiples of 80 (the copy is 16-B aligned), the pair
   // offsets of 8: each axis read is an 8-B aligned ds_read2_b64 (not an
   // unaligned ds_read_b128)
   __builtin_assume((node & 15) == 0);
-  __builtin_assume(((uint32_t)(uintptr_t)base & 15) == 0);
 #endif
   const E e = load_at<E>(base, node + 72);
   pl.en[0] = e.e[0];
@@ -1533,12 +1510,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       ln = S.n_root_items;
     } else {
       cur = 0;
-#if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_ABS
-      // the LDS-only binary walk addresses nodes by absolute LDS byte address
-      // (the staged entries hold them): the root is the copy's first byte
-      if constexpr (kFma && RT_SLAB_SIGN && RT_LDS_TRIPLE && (F & F_BVH4) == 0)
-        if (S.n_lds_nodes >= S.n_nodes) cur = (int)(uint32_t)(uintptr_t)lnodes;
-#endif
     }
     for (;;) {
       if constexpr ((F & F_BVH4) != 0) {
@@ -1635,13 +1606,8 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
               // between the two forms runs both slab passes in a mixed wave:
               // -6.5 %, profiles/r04b_arity_sign_ab.log, r04c_arity_sign_ab.log.)
               NodePlanes<2> pl;
-              if constexpr (RT_LDS_TRIPLE) { // cur: the node's byte offset / LDS address (entries staged so)
-#if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_ABS
-                load_planes_l(pl, (const RT_LDS char *)(uintptr_t)(uint32_t)cur, 0, po);
-#else
+              if constexpr (RT_LDS_TRIPLE) // cur: the node's byte offset (entries staged so)
                 load_planes_l(pl, (const RT_LDS char *)lnodes, cur, po);
-#endif
-              }
               else
                 load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
               slab2_planes(q, pl, tmin32, cl32, tn0, tn1, h0, h1);
@@ -1686,22 +1652,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
               e0 = N.entry[0];
               e1 = N.entry[1];
             }
-#if defined(__HIP_DEVICE_COMPILE__) && RT_VISIT_SELECT
-            {
-              // the three outcomes by selects, no branches: the far child is
-              // written above the stack whatever happens (a push only when both
-              // children are hit), the entry below it read whatever happens (a
-              // pop only when neither is; with an empty stack that read lands
-              // in other LDS and is discarded)
-              const bool n0 = h0 && (!h1 || tn0 <= tn1);
-              const int nr = n0 ? e0 : e1, fr = n0 ? e1 : e0;
-              const bool both = h0 && h1, none = !h0 && !h1, empty = top == stk;
-              *top = fr;
-              const int below = top[-64];
-              cur = none ? (empty ? -1 : below) : nr;
-              top += both ? 64 : (none && !empty ? -64 : 0);
-            }
-#else
             if (h0 && h1) {
               const bool first0 = tn0 <= tn1;
               push(first0 ? e1 : e0);
@@ -1711,7 +1661,6 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             } else {
               cur = pop();
             }
-#endif
             if (cur < -1 && ln == 0) { // first leaf: park it, keep walking
               lf = (~cur) >> 3;
               ln = (~cur) & 7;
@@ -1787,7 +1736,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
       if (sphere_root(s, lr, len2(lr.d), 0.001, kInf, t)) {
         V3 c0 = v3(s.c0[0] + 0 * s.dir[0], s.c0[1] + 0 * s.dir[1], s.c0[2] + 0 * s.dir[2]);
         double dist2 = len2(c0 - lr.o);
-        double ctm = sqrt_d(1 - s.rr / dist2);
+        double ctm = sqrt(1 - s.rr / dist2);
         double sa = 2 * kPi * (1 - ctm);
         p = 1 / sa;
       }
@@ -1799,7 +1748,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
         V3 n = ld3(q.n);
         V3 fn = dot(lr.d, n) < 0 ? n : -n;
         double d2 = t * t * len2(lr.d);
-        double cosine = fabs(dot(lr.d, fn) / sqrt_d(len2(lr.d)));
+        double cosine = fabs(dot(lr.d, fn) / sqrt(len2(lr.d)));
         p = d2 / (cosine * q.area);
       }
     }
@@ -1828,12 +1777,11 @@ RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double 
     V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
     V3 vv = unitv(cross(w, a));
     V3 uu = cross(w, vv);
-    double z = 1 + r2 * (sqrt_d(1 - s.rr / d2) - 1);
+    double z = 1 + r2 * (sqrt(1 - s.rr / d2) - 1);
     double sphi, cphi;
     sincos_2pi<KC>(r1, sphi, cphi);
-    const double sz = sqrt_d(1 - z * z);
-    double x = cphi * sz;
-    double y = sphi * sz;
+    double x = cphi * sqrt(1 - z * z);
+    double y = sphi * sqrt(1 - z * z);
     d = ((x * uu) + (y * vv)) + (z * w);
   } else if (L.kind == I_QUAD) { // Plane::random, Plane.cpp:128-132
     const DQuad &q = S.quads[L.idx];
