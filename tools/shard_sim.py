@@ -10,7 +10,9 @@ N>1 timed region runs besides the render: each rank's chunk sum
 speedup t(1) / max(rank) and the gather payload per rank.  The RCCL gather
 itself (1/N of the frame per rank over xGMI) is not included.
 
-    python tools/shard_sim.py [--config C2] [--reps 3]"""
+    python tools/shard_sim.py [--config C2] [--reps 3] [--n 1 2 4 8] [--units U ...]
+(--units: work-unit targets of the chunk choice, rtx.dist.auto_chunks; one
+line per N and target)"""
 import argparse
 import json
 import os
@@ -45,6 +47,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--n", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--units", type=int, nargs="+", default=[None])
     a = ap.parse_args()
     name, width, spp, depth = CONFIGS[a.config]
     S = load_scene(os.path.join(SCENES, name + ".json"))
@@ -54,9 +58,9 @@ def main():
     with Renderer(S) as R:
         t1 = timed(lambda: R.render_device(f, frame.data_ptr(), 0, output=abi.RT_OUT_SUM,
                                            accumulate=0), a.reps)
-        for N in (1, 2, 4, 8):
+        for N, U in [(N, U) for N in a.n for U in a.units]:
             n, t_r = tile_counts(f, N)
-            ch = auto_chunks(f, N)
+            ch = auto_chunks(f, N, U)
             buf = torch.empty((t_r, ch, 64, 3), dtype=torch.float64, device="cuda")
             sums = torch.empty((t_r, 64, 3), dtype=torch.float64, device="cuda")
             gath = torch.zeros((N, t_r, 64, 3), dtype=torch.float64, device="cuda")
@@ -75,7 +79,7 @@ def main():
                 st.append(timed(lambda: R.render_device(f, frame.data_ptr(), 0, samples=(b, e - b),
                                                         output=abi.RT_OUT_SUM, accumulate=0), a.reps))
             print(json.dumps({
-                "config": a.config, "N": N, "t1_ms": round(t1, 3), "tiles_chunks": ch,
+                "config": a.config, "N": N, "t1_ms": round(t1, 3), "units_target": U, "tiles_chunks": ch,
                 "tiles_rank_ms": [round(x, 3) for x in per_rank],
                 "tiles_chunk_sum_ms": None if ch == 1 else "included per rank",
                 "tiles_reorder_ms_rank0": round(t_frame, 3),
