@@ -246,9 +246,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   __shared__ double acc_lds[BW][64][3];
   // compacted leaf tests (BVH instances only; 1 KB per wave)
   __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? BW : 1];
-  // deferred noise albedos: owner rank -> lane (noise_wave; noise instances only)
-  constexpr bool kNoiseTab = (F & F_NOISE) != 0 && RT_NOISE_WAVE != 0 && RT_LDS_PERLIN != 0;
-  __shared__ NoiseLds noise_lds[kNoiseTab ? BW : 1];
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -397,26 +394,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     if (__ballot(ps.active) == 0) break;
     if (STATS) n_trips++; // converged here: every lane counts, lane 0 reports
     uint32_t v_trace = 0;
-    if constexpr (kNoiseTab) {
-      bool cont = true;
-      NoiseDefer nd;
-      nd.dn = -1;
-      if (ps.active) {
-        if (STATS) n_segments++;
-        const uint32_t nv0 = cnt.nodes;
-        cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
-            S, C, ps, key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp, &nd);
-        if (STATS) v_trace = cnt.nodes - nv0;
-      }
-      // converged: the trip's deferred noise albedos, the whole wave working
-      if (__ballot(nd.dn >= 0) != 0) noise_wave<STATS, F>(S, ps, nd, cnt, (RT_LDS NoiseLds *)&noise_lds[wv]);
-      if (ps.active && !cont) {
-        atomicAdd(&acc[ps.slot * 3 + 0], ps.T.x);
-        atomicAdd(&acc[ps.slot * 3 + 1], ps.T.y);
-        atomicAdd(&acc[ps.slot * 3 + 2], ps.T.z);
-        ps.active = false;
-      }
-    } else if (ps.active) {
+    if (ps.active) {
       if (STATS) n_segments++;
       const uint32_t nv0 = cnt.nodes;
       bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(

@@ -425,11 +425,6 @@ RT_HD double perlin_noise(PP P, V3 p) {
 #ifndef RT_LDS_PERLIN
 #define RT_LDS_PERLIN 1
 #endif
-// RT_NOISE_WAVE: noise albedos evaluated at the end of the path trip with the
-// octaves spread over the wave (noise_wave)
-#ifndef RT_NOISE_WAVE
-#define RT_NOISE_WAVE 1
-#endif
 using PerlinLds = DPerlin;
 #if defined(__HIP__)
 // The block's LDS copy of the scene's Perlin table (9 KB; allocated in the noise instances only -- the ones that call this).
@@ -1811,15 +1806,6 @@ struct PathState {
   int sample; // linear stratum index
   bool active;
 };
-// RT_NOISE_WAVE (noise instances, device): a scatter whose albedo is a noise
-// texture leaves T * (f1 * (f2 * albedo)) to noise_wave at the end of the
-// trip -- dn the texture (-1: none), dp the point, f1 = 1 / pdf, f2 = spdf.
-// One per trip, not part of PathState, so none of it is live across trips.
-struct NoiseDefer {
-  int dn;
-  V3 dp;
-  double f1, f2;
-};
 
 // Continue to the next segment unless the depth budget is spent (ray_color at
 // depth 0 returns 0, Camera.cpp:236-237; T * 0 keeps a NaN/inf weight alive).
@@ -1848,7 +1834,7 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 #endif
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
-                       const Hit &h, Counters &cnt, NoiseDefer *nd = nullptr) {
+                       const Hit &h, Counters &cnt) {
   const uint32_t b = ps.bounce;
   const DMat M = S.mats[h.mat];
   if (STATS) cnt.shade++;
@@ -1962,17 +1948,12 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   // albedo: fetched early when a noise texture may run (its long evaluation
   // overlaps less live state there), late otherwise (shorter live range)
   V3 att;
-  [[maybe_unused]] bool defer = false;
   if constexpr ((F & F_NOISE) != 0) {
-    if (STATS && S.texs[M.tex].kind == RT_TEX_NOISE) cnt.noise++;
-#if defined(__HIP_DEVICE_COMPILE__) && RT_NOISE_WAVE && RT_LDS_PERLIN
-    // the noise albedo from the LDS table: noise_wave evaluates it with the whole wave
-    defer = nd != nullptr && S.lds_perlin && S.texs[M.tex].kind == RT_TEX_NOISE;
-    if (!defer) att = tex_value<F>(S, M.tex, h.p);
-#else
-    if (STATS && S.texs[M.tex].kind == RT_TEX_NOISE) cnt.wnoise += wave_once();
+    if (STATS && S.texs[M.tex].kind == RT_TEX_NOISE) {
+      cnt.noise++;
+      cnt.wnoise += wave_once();
+    }
     att = tex_value<F>(S, M.tex, h.p);
-#endif
   }
   V3 w = kMerge ? u1 : unitv(h.n); // ONB(n), ONB.hpp:25-37
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
@@ -2040,88 +2021,17 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     return false;
   }
   if constexpr ((F & F_NOISE) == 0) att = tex_value<F>(S, M.tex, h.p);
-  if (defer) { // T * ((1 / pdf) * (spdf * albedo)) once noise_wave has the albedo
-    nd->dn = M.tex;
-    nd->dp = h.p;
-    nd->f1 = 1 / pdf;
-    nd->f2 = spdf;
-  } else {
-    V3 wgt = (1 / pdf) * (spdf * att);
-    ps.T = ps.T * wgt;
-  }
+  V3 wgt = (1 / pdf) * (spdf * att);
+  ps.T = ps.T * wgt;
   ps.ray = Ray{h.p, gd, r.tm};
   return advance(ps, C);
 }
-
-#if defined(__HIP__) && RT_LDS_PERLIN
-// The deferred noise albedos of a wave (RT_NOISE_WAVE), called where every lane
-// of the wave is active (the end of a path trip).  NoiseTexture's turb(p, 7) is
-// a sum of 7 octaves; here the n lanes that deferred one hand out their 7 n
-// octave evaluations to the whole wave, one per lane (ceil(7 n / 64) rounds
-// instead of 7 passes at n / 64 lane use), and each owner adds its octaves'
-// terms in octave order -- the same products and the same sums as the octave
-// loop, so the albedo is the same double.  Octave k: the noise at p * 2^k
-// weighted by 2^-k, exactly what k doublings / halvings give.  Only scenes
-// whose one Perlin table is in LDS defer (shade).  tab: 64 ints of per-wave
-// LDS (owner rank -> lane).
-// per-wave LDS of noise_wave (2.3 KB): owner rank -> lane, the owners' points,
-// one round's octave terms
-struct NoiseLds {
-  int tab[64];
-  double px[64], py[64], pz[64];
-  double term[64];
-};
-template <bool STATS, unsigned F>
-__device__ void noise_wave(const DScene &S, PathState &ps, const NoiseDefer &nd, Counters &cnt,
-                           RT_LDS NoiseLds *L) {
-  const bool own = nd.dn >= 0;
-  const uint64_t M = __ballot(own);
-  const int lane = (int)__lane_id();
-  const int r = __popcll(M & ((1ull << lane) - 1ull));
-  if (own) {
-    L->tab[r] = lane;
-    L->px[lane] = nd.dp.x;
-    L->py[lane] = nd.dp.y;
-    L->pz[lane] = nd.dp.z;
-  }
-  __builtin_amdgcn_wave_barrier();
-  const int total = 7 * __popcll(M);
-  double acc = 0.0;
-  for (int base = 0; base < total; base += 64) { // wave-uniform rounds
-    const int k = base + lane;
-    if (k < total) {
-      const int o = k / 7, oct = k - 7 * o;
-      const int src = L->tab[o];
-      const double m = (double)(1 << oct);
-      L->term[lane] = (1.0 / m) * perlin_noise(perlin_lds(), v3(L->px[src] * m, L->py[src] * m, L->pz[src] * m));
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (own) {
-      const int j0 = max(0, base - 7 * r), j1 = min(7, base + 64 - 7 * r);
-      for (int j = j0; j < j1; ++j) acc += L->term[7 * r + j - base]; // octave order
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (STATS && lane == 0) cnt.wnoise++;
-  }
-  if (own) {
-    const DTex &T = S.texs[nd.dn];
-#if RT_SIN_N
-    const double f = 1 + sin_n(T.scale * nd.dp.z + 10 * fabs(acc));
-#else
-    const double f = 1 + sin(T.scale * nd.dp.z + 10 * fabs(acc));
-#endif
-    const double a = f * 0.5; // the albedo f * (0.5, 0.5, 0.5), tex_value
-    const double w = nd.f1 * (nd.f2 * a);
-    ps.T = ps.T * v3(w, w, w);
-  }
-}
-#endif
 
 template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
                                         const Key &key, int *stk, const RT_LDS DNode *lnodes,
                                         Counters &cnt, RT_LDS LeafPool *pool = nullptr,
-                                        const LdsPrims &lp = LdsPrims{}, NoiseDefer *nd = nullptr) {
+                                        const LdsPrims &lp = LdsPrims{}) {
   Hit h;
   const uint64_t t0 = STATS ? clk() : 0;
   const bool hit = trace<STATS, F, LP>(S, ps.ray, h, key, ps.bounce, stk, lnodes, cnt, pool, lp);
@@ -2131,7 +2041,7 @@ RT_HD RT_FI bool segment(const DScene &S, const DCamera &C, PathState &ps,
     ps.T = ps.T * ld3(C.bg); // miss -> background (Camera.cpp:242-243)
     return false;
   }
-  const bool cont = shade<STATS, F>(S, C, ps, key, h, cnt, nd);
+  const bool cont = shade<STATS, F>(S, C, ps, key, h, cnt);
   if (STATS && wave_once()) cnt.cshade += clk() - t1;
   return cont;
 }
