@@ -113,15 +113,27 @@ def device_tiles_to_frame(gathered, frame, out):
     return out
 
 
+def shard_units(strata):
+    """Work-unit target of one rank: 32768 units (8 per wave slot) at 64 strata
+    per pixel, growing with sqrt(strata / 64) up to 4x -- the fastest of the
+    8-way sweeps on one GPU (profiles/r04q_shard_units_*.log,
+    r04v_shard_units_*.log): C2 (64 strata) 32768, C3 (256) 65536, C4 (1024)
+    and C5 (4096) 131072; RTX_SHARD_UNITS overrides."""
+    env = os.environ.get("RTX_SHARD_UNITS")
+    if env:
+        return int(env)
+    return int(32768 * min(4.0, max(1.0, (strata / 64.0) ** 0.5)))
+
+
 def auto_chunks(frame, world, target_units=None):
     """Stratum chunks per tile so one rank still has ~target_units wavefront work
     units (several per wave slot of the 256-CU chip): a rank of an 8-way split
     holds few tiles, and one wave per slot would make the slowest tile the
     kernel time."""
-    if target_units is None:
-        target_units = int(os.environ.get("RTX_SHARD_UNITS", "32768"))
     n, t_r = tile_counts(frame, world)
     strata = frame.sqrt_spp * frame.sqrt_spp
+    if target_units is None:
+        target_units = shard_units(strata)
     c = max(1, min(strata, -(-target_units // max(1, t_r))))
     cs = -(-strata // c)  # strata per chunk; no empty chunks
     return -(-strata // cs)

@@ -136,6 +136,25 @@ def test_tiles_to_frame_reorders_ragged_frames():
         assert np.array_equal(got, img)
 
 
+def test_shard_chunks_follow_the_strata(monkeypatch):
+    """8-way tile shards: the work-unit target grows with the strata per pixel
+    (profiles/r04q_shard_units_*.log, r04v_shard_units_*.log) and the chunk
+    count leaves no empty chunk; RTX_SHARD_UNITS overrides."""
+    from rtx.dist import auto_chunks, shard_units
+    from rtx.render import camera_frame
+    monkeypatch.delenv("RTX_SHARD_UNITS", raising=False)
+    assert [shard_units(s) for s in (16, 64, 256, 1024, 4096)] == [32768, 32768, 65536, 131072, 131072]
+    S = load_scene(SCENE)
+    for spp, want in ((64, 8), (256, 16), (1024, 32)):  # C2 / C3 / C4 at 1080p, 8 ranks
+        f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=spp, max_depth=8))
+        c = auto_chunks(f, 8)
+        strata = f.sqrt_spp ** 2
+        cs = -(-strata // c)
+        assert c == want and (c - 1) * cs < strata
+    monkeypatch.setenv("RTX_SHARD_UNITS", "4096")
+    assert shard_units(256) == 4096
+
+
 def _tile_worker(rank, world, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
