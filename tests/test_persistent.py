@@ -91,3 +91,39 @@ def test_persistent_tile_subset_launch(layout_chunks):
     pers, single = run(1), run(1000000)
     assert np.array_equal(pers, single)
     assert pers.any()
+
+
+def test_staged_tree_forms_render_the_same_frame():
+    """C3's scene in the persistent instance with the whole tree staged in LDS
+    (80-B DNodeL nodes, child entries as byte offsets, the sign-picked visit),
+    with only a prefix staged (DNodeL prefix + DNode table in HBM, the min/max
+    visit) and with nothing staged: the three walks visit the same nodes in the
+    same order (the sign-picked planes ARE the min/max picks, rt_path.h), so
+    the frames are bit-identical -- and match the oracle."""
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    cam = S.camera_desc(image_width=64, samples_per_pixel=16, max_depth=8)
+    f = camera_frame(cam)
+    frames, infos = {}, {}
+    for staged in ("all", "100", "0"):
+        env = {"RT_GRID_CAP": "3"}
+        if staged != "all":
+            env["RTX_LDS_NODES_PC"] = staged
+        old = {k: os.environ.get(k) for k in list(env) + ["RTX_LDS_NODES_PC"]}
+        os.environ.pop("RTX_LDS_NODES_PC", None)
+        os.environ.update(env)
+        try:
+            with Renderer(S) as R:
+                infos[staged] = R.info()
+                frames[staged] = R.render(f, seed=9)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    assert infos["all"]["lds_nodes_persistent"] == infos["all"]["n_nodes"]
+    assert infos["100"]["lds_nodes_persistent"] == 100 and infos["0"]["lds_nodes_persistent"] == 0
+    assert np.array_equal(frames["all"], frames["100"])
+    assert np.array_equal(frames["all"], frames["0"])
+    ref = O.oracle_render(S, cam, O.MODE_COUNTER, 9)
+    assert np.abs(frames["all"] - ref).max() <= 1e-4
