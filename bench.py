@@ -769,6 +769,11 @@ def main():
     if st.get("wave_noise_iters"):
         roof["lane_utilisation"]["noise_albedo"] = round(
             st["noise_evals"] / (64 * st["wave_noise_iters"]), 4)
+    if st.get("medium_box_tests"):
+        # box-boundary media: share of their lanes box_span deferred to the
+        # general boundary scan (edge / corner / parallel rays)
+        roof["lane_utilisation"]["medium_box_deferred"] = round(
+            st["medium_box_deferred"] / st["medium_box_tests"], 6)
     if st.get("model_trace_max"):
         # the node-loop SIMD model (STATS): one walk per lane per trip vs each
         # lane's walks of two consecutive trips back to back (two walks per lane)

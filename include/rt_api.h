@@ -70,7 +70,7 @@ extern "C" {
       LDS fields.
    3: rt_tiles_sum_device, rt_tiles_to_frame_device, rt_multi_gather_ms; the
       rt_multi exchange runs on the devices. */
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define RT_OK 0
@@ -293,6 +293,11 @@ typedef struct rt_path_stats {
      NoiseTexture): lanes, and wavefront executions of that evaluation (their
      ratio / 64 is the evaluation's lane use). */
   uint64_t noise_evals, wave_noise_iters;
+  /* Constant media with a box boundary (make_box): lanes whose boundary
+     queries took the six-face slab form, and lanes of those it deferred to
+     the general boundary scan (edge / corner / parallel rays within its
+     margin; ABI 4). */
+  uint64_t medium_box_tests, medium_box_deferred;
 } rt_path_stats;
 
 typedef struct rt_scene_info {
@@ -325,6 +330,8 @@ typedef struct rt_scene_info {
                                      per CU) or 4 (traversal stacks too deep for 16); 0: none */
   int32_t lds_perlin; /* 1: the scene's Perlin table (one noise texture source) is staged in
                          LDS by every block of the noise instances; 0: read from HBM */
+  int32_t lds_node_bytes; /* bytes per BVH node as staged in LDS (DNodeL 80 / DNode4 128;
+                             node_bytes is the HBM layout's, ABI 4) */
 } rt_scene_info;
 
 typedef struct rt_scene rt_scene; /* opaque, library-owned */

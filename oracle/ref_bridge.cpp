@@ -449,6 +449,32 @@ int ref_object_hit(const rt_scene_desc *d, int obj, const double ray[7], double 
   return 1;
 }
 
+/* The two boundary queries of ConstantMedium::hit (ConstantMedium.cpp:28-32)
+   for medium object `obj` on n rays (x, y, z, dx, dy, dz, time): the
+   boundary's own hit over UNIVERSE_INTERVAL, then over (t1 + 0.0001, INF).
+   out per ray: first hit?, t1, second hit?, t2 (0 where not reached). */
+int ref_medium_boundary(const rt_scene_desc *d, int obj, const double *rays, int n, double *out) {
+  Graph g;
+  g.load(d);
+  auto cm = std::dynamic_pointer_cast<ConstantMedium>(g.object(obj));
+  if (!cm) return -1;
+  HittablePtr b = cm->get_boundary();
+  for (int k = 0; k < n; ++k) {
+    const double *q = rays + 7 * k;
+    Ray r(Point3(q[0], q[1], q[2]), Vec3(q[3], q[4], q[5]), q[6]);
+    HitRecord rec1, rec2;
+    double *o = out + 4 * k;
+    o[0] = o[1] = o[2] = o[3] = 0.0;
+    if (!b->hit(r, UNIVERSE_INTERVAL, rec1)) continue;
+    o[0] = 1.0;
+    o[1] = rec1.t;
+    if (!b->hit(r, Interval(rec1.t + 0.0001, INF), rec2)) continue;
+    o[2] = 1.0;
+    o[3] = rec2.t;
+  }
+  return 0;
+}
+
 double ref_object_pdf(const rt_scene_desc *d, int obj, const double org[3], const double dir[3]) {
   Graph g;
   g.load(d);

@@ -557,6 +557,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   in.lds_prims_persistent = d.lds_items_pc > 0;
   in.persistent_block_waves = d.pc_waves;
   in.lds_perlin = d.lds_perlin;
+  in.lds_node_bytes = RT_LDS_NODE_BYTES(d.features);
   *out = s;
   return RT_OK;
 }
@@ -815,6 +816,8 @@ int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
   stats->model_trace_pair_max = h[19];
   stats->noise_evals = h[20];
   stats->wave_noise_iters = h[21];
+  stats->medium_box_tests = h[22];
+  stats->medium_box_deferred = h[23];
   return RT_OK;
 }
 
@@ -964,10 +967,22 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
   for (int d = 1; d < n_devices && d < n_shards; ++d) {
     if (devices[d] == root) continue;
     int can = 0;
-    if (hipDeviceCanAccessPeer(&can, devices[d], root) == hipSuccess && can) {
+    const hipError_t ce = hipDeviceCanAccessPeer(&can, devices[d], root);
+    if (ce != hipSuccess) (void)hipGetLastError();
+    if (ce == hipSuccess && can) {
       DeviceGuard g(devices[d]);
-      hipError_t e = hipDeviceEnablePeerAccess(root, 0);
-      if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      const hipError_t e = hipDeviceEnablePeerAccess(root, 0);
+      // any failure (already enabled or not) leaves no direct peer access to
+      // rely on: the peer copies then stage through the host.  Clear the
+      // thread's last error so the first multi frame's launch checks do not
+      // report it.
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        if (e != hipErrorPeerAccessAlreadyEnabled)
+          fprintf(stderr, "rt_multi_create: no peer access from device %d to %d (%s); "
+                          "peer copies stage through the host\n",
+                  devices[d], root, hipGetErrorString(e));
+      }
     }
   }
   *out = m;

@@ -477,7 +477,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
                                         lane == 0 ? cyc_loop : 0u, lane == 0 ? cyc_regen : 0u,
                                         cnt.ctrace, cnt.cmedia, cnt.cshade, cnt.clights,
                                         lane == 0 ? m_single : 0u, lane == 0 ? m_pair : 0u,
-                                        cnt.noise, cnt.wnoise};
+                                        cnt.noise, cnt.wnoise, cnt.mbox, cnt.mbox_fb};
     for (int k = 0; k < RT_N_STATS; ++k) {
       unsigned long long x = v[k];
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);

@@ -26,7 +26,7 @@
 #include <stdint.h>
 
 #define RT_MAX_CHAIN 4    // RotateY/Translate ops above a leaf item
-#define RT_N_STATS 22      // counters of the STATS kernel instance (rt_path_stats)
+#define RT_N_STATS 24      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 #define RT_STACK_DEPTH4 64 // 4-wide walks push up to three entries per level
 #ifndef RT_PC_WAVES
@@ -85,7 +85,20 @@ struct DMedium {     // ConstantMedium: -1/density, phase material, boundary ite
   double neg_inv_density;
   int32_t phase, id;
   int32_t b_first, b_count; // boundary items in bitems[] (medium-local frame)
+  // box = 1: the boundary is make_box's six axis-aligned quads (PlaneUtility.hpp:
+  // 11-39), all under the one transform chain [bxf_first, +bxf_count), two faces
+  // per axis whose rectangles span the other two axes' face planes (checked by
+  // the scene compiler, rt_scene.cpp box_of).  rt_path.h box_span then answers
+  // both boundary queries from the six face distances alone.  Per axis a and
+  // face f (the two faces normal to a): the face's unit-normal component
+  // bnk[a][f] = Plane::m_normal[a] (|bnk[a][0]| == |bnk[a][1]|) and its
+  // bD[a][f] = Plane::m_D; bB[a] = the largest |plane coordinate| along a.
+  int32_t box, bxf_first, bxf_count, pad_;
+  double bnk[3][2];
+  double bD[3][2];
+  double bB[3];
 };
+static_assert(sizeof(DMedium) == 160, "DMedium layout");
 
 struct DNode {       // 64 B: both children's boxes (fp32, rounded outward) + links
   float lo[3][2];    // lo[axis][child]: the two children's planes of one axis side by

@@ -788,15 +788,114 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
   return items_closest_t(S, S.bitems, M.b_first, M.b_count, r, thr, kInf, t2);
 }
 
+// Both boundary queries of ConstantMedium::hit for a make_box boundary
+// (DMedium::box), from the six face distances alone -- the same doubles as
+// boundary_span's, at a third of its work.  Returns 1 (span: t1, t2 set), 0 (no
+// span: boundary_span would return false) or -1 (undecided here: the caller runs
+// boundary_span).  `r` is the medium-frame ray; the boundary's own chain is
+// applied here.
+//
+// 1. Exact face distances.  Plane::hit's t for a face normal to axis a is
+//    RN(RN(D - RN(n_a o_a)) / RN(n_a d_a)) (its dot products with the unit
+//    normal's exact zeros drop out, as in quad_t_aa).  Both faces of an axis
+//    have |n_a| equal, so their denominators are b and +-b exactly, and one
+//    correctly rounded reciprocal y = RN(1/b) (rcp_n) gives each quotient by
+//    Markstein's correction (div_mk) -- the division's own double as long as
+//    |x| >= 2^-960 or x = 0, and |x/b| < 2^1000.  The lane check `ok`
+//    guarantees that: 1e-8 <= |b| <= 2^90 (1e-8 is Plane::hit's own parallel
+//    test, so no face is skipped here that the reference would test), |o_a| <=
+//    2^90 and o_a = 0 or |o_a| >= 2^-898, and the scene compiler admits only
+//    |D| in {0} U [2^-900, 2^90] and |n_a| in [0.5, 2]: then D and RN(n_a o_a)
+//    are both 0 or multiples of 2^-952, so x is 0 or |x| >= 2^-952.  Any other
+//    lane (non-finite rays included: every check fails on NaN) returns -1.
+// 2. Which faces pass Plane::hit's interior test.  The six distances form a
+//    slab test: per axis tn = min, tf = max of its two faces; entry = max tn,
+//    exit = min tf.  A face's hit point lies inside the box's extent along
+//    another axis c exactly when its t lies in [tn_c, tf_c] -- in real
+//    arithmetic.  Plane::hit decides it on rounded values: the t's above carry
+//    relative errors of ~2^-52 in (B_a + |o_a|) / |d_a| (B_a: the box's largest
+//    |plane coordinate| along a), the interior test's point, alpha / beta
+//    (RN(w (pv x v))) and the rectangle edges (Q + u vs. the other axis's plane:
+//    the compiler admits at most 2^-48 B apart) another ~2^-50 (B_c + |o_c| +
+//    |t d_c|) / |d_c| in t.  With s_a = (B_a + |o_a|) |y_a| (|y_a| >= 1 / (2
+//    |d_a|)) every such error is below 2^-45 (s_0 + s_1 + s_2), 32x below the
+//    margin del = 2^-40 (s_0 + s_1 + s_2).  So, with del:
+//    * every near face but the entry axis's, t < entry - del: its point lies
+//      before the entry axis's slab -- fails; likewise every far face but the
+//      exit axis's, t > exit + del -- fails (cn, cf: exactly one face each
+//      within del of entry / exit, else -1);
+//    * entry < exit - del: the entry and exit faces pass (their points lie
+//      inside the other two slabs by more than del), and only they: the
+//      candidates are {entry, exit};
+//    * entry > exit + del: no face passes (the entry face lies beyond the exit
+//      axis's slab and vice versa);
+//    * otherwise -1.
+// 3. boundary_span's candidate rules on {entry, exit} (two quads: closed
+//    intervals): t1 = entry, t2 = the first candidate >= RN(t1 + 0.0001).
+// Proven on the host against the reference's own ConstantMedium boundary
+// queries (tests/test_medium_box.py: edge, corner, grazing and axis-parallel
+// rays, oracle/_ref) and on the device against boundary_span bit for bit.
+#ifndef RT_BOX_SPAN
+#define RT_BOX_SPAN 1
+#endif
+RT_HD RT_FI int box_span(const DScene &S, const DMedium &M, const Ray &mr, double &t1,
+                         double &t2) {
+  const Ray r = M.bxf_count ? to_local(S, M.bxf_first, M.bxf_count, mr) : mr;
+  double tn[3], tf[3], s = 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double o = comp(r.o, a), d = comp(r.d, a);
+    const double n0 = M.bnk[a][0], n1 = M.bnk[a][1];
+    const double b = n0 * d; // RN(n_a d_a): face 0's denominator; face 1's is +-b
+    const double ab = fabs(b), ao = fabs(o);
+    ok = ok && ab >= 1e-8 && ab <= 0x1p90 && ao <= 0x1p90 && (o == 0.0 || ao >= 0x1p-898);
+    const double y = rcp_n(b); // |b| in [1e-8, 2^90]: correctly rounded
+    const double x0 = M.bD[a][0] - n0 * o, x1 = M.bD[a][1] - n1 * o;
+    const double u0 = div_mk(x0, b, y);
+    const double u1 = (n1 == n0) ? div_mk(x1, b, y) : div_mk(x1, -b, -y);
+    tn[a] = fmin(u0, u1);
+    tf[a] = fmax(u0, u1);
+    s += (M.bB[a] + ao) * fabs(y);
+  }
+  if (!ok) return -1;
+  const double entry = fmax(fmax(tn[0], tn[1]), tn[2]);
+  const double exit_ = fmin(fmin(tf[0], tf[1]), tf[2]);
+  const double del = 0x1p-40 * s;
+  const double elo = entry - del, xhi = exit_ + del;
+  const int cn = (tn[0] >= elo) + (tn[1] >= elo) + (tn[2] >= elo);
+  const int cf = (tf[0] <= xhi) + (tf[1] <= xhi) + (tf[2] <= xhi);
+  if (cn != 1 || cf != 1) return -1;
+  if (entry > xhi) return 0;
+  if (!(entry < exit_ - del)) return -1;
+  t1 = entry;
+  const double thr = entry + 0.0001;
+  if (thr <= entry) { // |entry| >= 2^39: the closed interval keeps t1 itself
+    t2 = entry;
+    return 1;
+  }
+  if (thr <= exit_) {
+    t2 = exit_;
+    return 1;
+  }
+  return 0;
+}
+
 // ConstantMedium::hit (ConstantMedium.cpp:25-94) in the medium's local frame:
 // the scattering distance only (hit_t); medium_record builds the record of
 // the winning medium once, after every medium has been tested.
+// (box_path, STATS: 1 box_span decided, 0 box_span deferred to boundary_span,
+// -1 not a box)
 RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin,
-                    double tmax, const Key &key, uint32_t bounce, double &hit_t) {
+                    double tmax, const Key &key, uint32_t bounce, double &hit_t,
+                    int &box_path) {
   const DMedium M = S.media[it.idx];
   Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
   double t1, t2;
-  if (!boundary_span(S, M, r, t1, t2)) return false;
+  const int rc = (RT_BOX_SPAN && M.box) ? box_span(S, M, r, t1, t2) : -2;
+  box_path = rc == -2 ? -1 : rc >= 0;
+  if (rc == 0) return false;
+  if (rc < 0 && !boundary_span(S, M, r, t1, t2)) return false;
   if (t1 < tmin) t1 = tmin;
   if (t2 > tmax) t2 = tmax;
   if (t1 >= t2) return false;
@@ -1181,6 +1280,7 @@ struct Counters {
   uint32_t wnode, wleaf, wshade; // wave-level iterations (counted by one lane per wave)
   uint64_t ctrace, cmedia, cshade, clights; // wave-level cycles (first active lane adds)
   uint32_t noise, wnoise; // noise-texture albedo evaluations: lanes, wave executions
+  uint32_t mbox, mbox_fb; // box-boundary medium tests: lanes, lanes box_span deferred
 };
 // shader clock for the STATS instance's phase cycles (s_memtime)
 RT_HD RT_FI uint64_t clk() {
@@ -1277,7 +1377,13 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
         continue;
       if (STATS) cnt.other++;
       double tm_hit;
-      if (medium_t(S, S.mitems[m], r, tmin, closest, key, bounce, tm_hit)) {
+      int box_path;
+      const bool mh = medium_t(S, S.mitems[m], r, tmin, closest, key, bounce, tm_hit, box_path);
+      if (STATS) {
+        cnt.mbox += box_path >= 0;
+        cnt.mbox_fb += box_path == 0;
+      }
+      if (mh) {
         closest = tm_hit;
         cl32 = f32_up(closest);
         best_m = m;

@@ -670,6 +670,63 @@ struct Compiler {
     return b;
   }
 
+  // A medium boundary that is a box (make_box, PlaneUtility.hpp:11-39): six
+  // axis-aligned quads under one transform chain, two normal to each axis, each
+  // face's rectangle spanning the other two axes' face planes.  Sets DMedium::box
+  // and the per-axis face constants rt_path.h box_span reads; box_span's range
+  // and margin argument needs |D| in {0} U [2^-900, 2^90], |n_a| in [0.5, 2] and
+  // equal for both faces of an axis, and rectangle edges within 2^-48 B of the
+  // planes (B: the largest |plane coordinate| on that axis).  Anything else
+  // keeps the general boundary scan (box = 0).
+  void box_of(DMedium &m, const std::vector<DItem> &bs) {
+    m.box = 0;
+    if (bs.size() != 6) return;
+    int nface[3] = {0, 0, 0};
+    const DQuad *face[3][2] = {};
+    for (const DItem &b : bs) {
+      if (b.kind != I_QUAD || b.xf_first != bs[0].xf_first || b.xf_count != bs[0].xf_count) return;
+      const DQuad &q = H.quads[b.idx];
+      if (q.aa < 0) return;
+      const int k = q.aa & 3;
+      if (nface[k] == 2) return;
+      face[k][nface[k]++] = &q;
+    }
+    double P[3][2];
+    for (int a = 0; a < 3; ++a) {
+      if (nface[a] != 2) return;
+      for (int f = 0; f < 2; ++f) {
+        const DQuad &q = *face[a][f];
+        const double n = q.n[a], D = q.D, aD = std::fabs(D);
+        if (!(std::fabs(n) >= 0.5 && std::fabs(n) <= 2.0)) return;
+        if (!(D == 0.0 || (aD >= 0x1p-900 && aD <= 0x1p90))) return;
+        P[a][f] = D / n; // the face's plane coordinate along a
+        m.bnk[a][f] = n;
+        m.bD[a][f] = D;
+      }
+      if (std::fabs(m.bnk[a][0]) != std::fabs(m.bnk[a][1]) || !(P[a][0] != P[a][1])) return;
+      m.bB[a] = std::fmax(std::fabs(P[a][0]), std::fabs(P[a][1]));
+    }
+    // every face's rectangle spans the other axes' planes: along its u axis i,
+    // {Q_i, Q_i + u_i} = the planes of axis i; along v likewise
+    for (int a = 0; a < 3; ++a)
+      for (int f = 0; f < 2; ++f) {
+        const DQuad &q = *face[a][f];
+        const int ax[2] = {(q.aa >> 2) & 3, (q.aa >> 4) & 3};
+        const double *side[2] = {q.u, q.v};
+        for (int e = 0; e < 2; ++e) {
+          const int i = ax[e];
+          const double lo = std::fmin(P[i][0], P[i][1]), hi = std::fmax(P[i][0], P[i][1]);
+          const double e0 = q.Q[i], e1 = q.Q[i] + side[e][i];
+          const double tol = 0x1p-48 * m.bB[i];
+          if (!(std::fabs(std::fmin(e0, e1) - lo) <= tol && std::fabs(std::fmax(e0, e1) - hi) <= tol))
+            return;
+        }
+      }
+    m.box = 1;
+    m.bxf_first = bs[0].xf_first;
+    m.bxf_count = bs[0].xf_count;
+  }
+
   bool make_item(const FItem &f, DItem &it, Bx &bb) {
     std::memset(&it, 0, sizeof it);
     const rt_object_desc &x = D->objects[f.obj];
@@ -700,6 +757,7 @@ struct Compiler {
       }
       m.b_first = (int32_t)H.bitems.size();
       m.b_count = (int32_t)tmp.size();
+      box_of(m, tmp);
       for (auto &bi : tmp) H.bitems.push_back(bi);
       it.idx = (int32_t)H.media.size();
       H.media.push_back(m);

@@ -28,7 +28,10 @@
 // description as JSON and exit; used by tests/test_cli.py), and the multi-GPU
 // flags SURVEY §5 adds: --gpus N renders on devices device..device+N-1 through
 // rt_multi_* (one host thread and one scene per shard, 8x8 tiles dealt
-// round-robin, tile sums gathered on the host); --shards K (default N) splits
+// round-robin; each shard sums its chunk partials on its own device, its tiles
+// are peer-copied to the first shard's device -- xGMI between GPUs -- and
+// reordered into the frame there, one D2H copy per frame: rt_api.cpp
+// rt_multi_render); --shards K (default N) splits
 // the frame into K tile shards, K > N putting several shards on one device.
 // The sharded frame is bit-identical to the one-device frame (rt_api.h).
 #include "rt_api.h"

@@ -5,7 +5,7 @@ sizes against the compiled library's own view (rt_abi_sizes) when available.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 3  # include/rt_api.h; rtx/lib.py refuses a library of another version
+RT_ABI_VERSION = 4  # include/rt_api.h; rtx/lib.py refuses a library of another version
 
 RT_OK = 0
 RT_ERR_INVALID = -1
@@ -105,7 +105,8 @@ class PathStats(C.Structure):
         "other_tests", "light_tests", "shade_events",
         "wave_trips", "wave_node_iters", "wave_leaf_iters", "wave_shade_iters",
         "cyc_loop", "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights",
-        "model_trace_max", "model_trace_pair_max", "noise_evals", "wave_noise_iters")]
+        "model_trace_max", "model_trace_pair_max", "noise_evals", "wave_noise_iters",
+        "medium_box_tests", "medium_box_deferred")]
 
 
 class SceneInfo(C.Structure):
@@ -119,7 +120,8 @@ class SceneInfo(C.Structure):
                 ("stack_depth", C.c_int32), ("lds_fixed_bytes", C.c_int32),
                 ("lds_block_budget", C.c_int32), ("waves_per_simd", C.c_int32),
                 ("lds_nodes_persistent", C.c_int32), ("lds_prims_persistent", C.c_int32),
-                ("persistent_block_waves", C.c_int32), ("lds_perlin", C.c_int32)]
+                ("persistent_block_waves", C.c_int32), ("lds_perlin", C.c_int32),
+                ("lds_node_bytes", C.c_int32)]
 
 
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).

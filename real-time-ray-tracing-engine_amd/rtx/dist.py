@@ -104,8 +104,15 @@ def device_tiles_to_frame(gathered, frame, out):
     [H, W, 3] on the device (rt_tiles_to_frame_device)."""
     from .lib import check, load
     from .render import Renderer
+    import torch
     assert gathered.is_cuda and out.is_cuda and gathered.is_contiguous() and out.is_contiguous()
+    # the kernel reads both as doubles, gathered as [world][T_r][64][3] with
+    # tile t at (t % world, t // world)
+    assert gathered.dtype == out.dtype == torch.float64
+    assert gathered.dim() == 4 and tuple(gathered.shape[2:]) == (64, 3)
     assert out.shape == (frame.image_height, frame.image_width, 3)
+    n_tiles = ((frame.image_width + 7) // 8) * ((frame.image_height + 7) // 8)
+    assert gathered.shape[1] >= (n_tiles + gathered.shape[0] - 1) // gathered.shape[0]
     p = Renderer.params(output=abi.RT_OUT_SUM)
     check(load().rt_tiles_to_frame_device(C.c_void_p(gathered.data_ptr()), gathered.shape[0],
                                           gathered.shape[1], C.byref(frame), C.byref(p),

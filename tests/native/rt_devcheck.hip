@@ -6,10 +6,17 @@
 //   rcp_n(x)            vs 1.0 / x      (returned in the div_mk slot when b == 0)
 //   sincos_2pi<1>, <2>  vs sincos_2pi<0> (the polynomial constants materialised at
 //                       their use in SGPRs / VGPRs vs held, rt_path.h RT_KCONST)
+//   box_span            vs boundary_span (a make_box medium's boundary queries,
+//                       tests/test_medium_box.py; the scene compiled on the host
+//                       by csrc/rt_scene.cpp, linked in)
 // Nothing on the product path links this.
 #include <hip/hip_runtime.h>
 
 #include "../../real-time-ray-tracing-engine_amd/csrc/rt_path.h"
+#include "../../real-time-ray-tracing-engine_amd/csrc/rt_scene.h"
+
+#include <string>
+#include <vector>
 
 namespace {
 __global__ void arith_kernel(const double *x, const double *b, int n, double *sq_n, double *sq,
@@ -41,7 +48,67 @@ __global__ void sincos_kernel(const double *u, int n, double *out) { // out: [6]
   out[4 * n + k] = s2;
   out[5 * n + k] = c2;
 }
+// one ray per thread: out[6] as emu_medium_spans (tests/native/rt_emulate.cpp)
+__global__ void medium_kernel(DScene S, int m, const double *rays, int n, double *out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const DMedium M = S.media[m];
+  const double *q = rays + 7 * k;
+  rtp::Ray r{rtp::v3(q[0], q[1], q[2]), rtp::v3(q[3], q[4], q[5]), q[6]};
+  double a1 = 0, a2 = 0, g1 = 0, g2 = 0;
+  const int rc = M.box ? rtp::box_span(S, M, r, a1, a2) : -2;
+  const bool g = rtp::boundary_span(S, M, r, g1, g2);
+  double *o = out + 6 * k;
+  o[0] = rc;
+  o[1] = rc == 1 ? a1 : 0.0;
+  o[2] = rc == 1 ? a2 : 0.0;
+  o[3] = g ? 1.0 : 0.0;
+  o[4] = g ? g1 : 0.0;
+  o[5] = g ? g2 : 0.0;
+}
 } // namespace
+
+template <class T>
+static int upload(const std::vector<T> &v, void **d) {
+  *d = nullptr;
+  if (v.empty()) return 0;
+  if (hipMalloc(d, v.size() * sizeof(T)) != hipSuccess) return -1;
+  return hipMemcpy(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess ? 0 : -2;
+}
+
+// Both boundary queries of medium m on n medium-frame rays, on the device:
+// out per ray as emu_medium_spans.  Returns 0, or a negative code.
+extern "C" int devcheck_medium_spans(const rt_scene_desc *desc, int m, const double *rays, int n,
+                                     double *out) {
+  rtx::HostScene H;
+  std::string err;
+  if (rtx::compile_scene(desc, H, err) != RT_OK) return -10;
+  if (m < 0 || m >= (int)H.media.size() || n <= 0) return -11;
+  void *b[7] = {};
+  int rc = upload(H.bitems, &b[0]);
+  if (!rc) rc = upload(H.xforms, &b[1]);
+  if (!rc) rc = upload(H.spheres, &b[2]);
+  if (!rc) rc = upload(H.quads, &b[3]);
+  if (!rc) rc = upload(H.media, &b[4]);
+  if (!rc) rc = upload(std::vector<double>(rays, rays + 7 * (size_t)n), &b[5]);
+  if (!rc && hipMalloc(&b[6], 6 * sizeof(double) * (size_t)n) != hipSuccess) rc = -3;
+  if (!rc) {
+    DScene S{};
+    S.bitems = (const DItem *)b[0];
+    S.xforms = (const DXform *)b[1];
+    S.spheres = (const DSphere *)b[2];
+    S.quads = (const DQuad *)b[3];
+    S.media = (const DMedium *)b[4];
+    hipLaunchKernelGGL(medium_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, S, m,
+                       (const double *)b[5], n, (double *)b[6]);
+    if (hipDeviceSynchronize() != hipSuccess) rc = -4;
+  }
+  if (!rc && hipMemcpy(out, b[6], 6 * sizeof(double) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = -5;
+  for (void *p : b)
+    if (p) (void)hipFree(p);
+  return rc;
+}
 
 // sincos_2pi's three constant forms on the device: out [6][n] = s0, c0, s1, c1, s2, c2
 extern "C" int devcheck_sincos(const double *u, int n, double *out) {

@@ -87,8 +87,10 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   S.n_root_items = H.n_root_items;
   S.features = features;
   S.static_spheres = rtx::all_spheres_static(H);
-  S.stack_depth = bvh4 ? rtx::bvh4_stack_depth(depth4)
-                       : std::max(1, std::min(H.bvh_depth + 1, RT_STACK_DEPTH));
+  // rt_scene_create's rule: the walk pushes with no overflow check, so a tree
+  // deeper than the stack is refused, not clamped
+  S.stack_depth = bvh4 ? rtx::bvh4_stack_depth(depth4) : std::max(1, H.bvh_depth + 1);
+  if (S.stack_depth > (bvh4 ? RT_STACK_DEPTH4 : RT_STACK_DEPTH)) return -2;
   S.n_lds_nodes = S.n_nodes; // host: the whole tree is the "LDS" copy
   // in the form the kernel stages it: DNode4 as is, binary nodes as DNodeL
   std::vector<DNodeL> lnodes_l;
@@ -265,6 +267,41 @@ extern "C" int emu_quad_forms(const rt_scene_desc *desc, const double *o, const 
     out[4 * k + 1] = h0 ? t0 : 0.0;
     out[4 * k + 2] = h1;
     out[4 * k + 3] = h1 ? t1 : 0.0;
+  }
+  return 0;
+}
+
+// Both boundary queries of ConstantMedium::hit for medium m (index into the
+// compiled media, in scene order) on n medium-frame rays (x, y, z, dx, dy, dz,
+// time), through the kernel source's box_span (make_box boundaries) and its
+// general boundary_span.  out per ray: box_span's code (1 span, 0 none, -1
+// deferred, -2 not a box), its t1, t2, then boundary_span's result (1 / 0), t1, t2.
+extern "C" int emu_medium_spans(const rt_scene_desc *desc, int m, const double *rays, int n,
+                                double *out) {
+  rtx::HostScene H;
+  std::string err;
+  if (rtx::compile_scene(desc, H, err) != RT_OK) return -1;
+  if (m < 0 || m >= (int)H.media.size()) return -2;
+  DScene S{};
+  S.bitems = H.bitems.data();
+  S.xforms = H.xforms.data();
+  S.spheres = H.spheres.data();
+  S.quads = H.quads.data();
+  S.media = H.media.data();
+  const DMedium &M = H.media[m];
+  for (int k = 0; k < n; ++k) {
+    const double *q = rays + 7 * k;
+    Ray r{v3(q[0], q[1], q[2]), v3(q[3], q[4], q[5]), q[6]};
+    double *o = out + 6 * k;
+    double a1 = 0, a2 = 0, g1 = 0, g2 = 0;
+    const int rc = M.box ? box_span(S, M, r, a1, a2) : -2;
+    const bool g = boundary_span(S, M, r, g1, g2);
+    o[0] = rc;
+    o[1] = rc == 1 ? a1 : 0.0;
+    o[2] = rc == 1 ? a2 : 0.0;
+    o[3] = g ? 1.0 : 0.0;
+    o[4] = g ? g1 : 0.0;
+    o[5] = g ? g2 : 0.0;
   }
   return 0;
 }

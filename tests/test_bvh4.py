@@ -105,7 +105,9 @@ def test_bvh4_kept_binary_when_its_stacks_do_not_fit_lds():
     assert i4["bvh_arity"] == 4 and i4["stack_depth"] > i2["stack_depth"]
     for i in (i2, i4):
         assert i["lds_fixed_bytes"] <= i["lds_block_budget"] <= 65536
-        assert i["lds_fixed_bytes"] + i["lds_nodes"] * i["node_bytes"] <= i["lds_block_budget"]
+        # the staged node size (DNodeL 80 B for binary trees), not the HBM DNode's 64
+        assert i["lds_node_bytes"] == (128 if i["bvh_arity"] == 4 else 80)
+        assert i["lds_fixed_bytes"] + i["lds_nodes"] * i["lds_node_bytes"] <= i["lds_block_budget"]
     assert i4["lds_fixed_bytes"] > i2["lds_fixed_bytes"]
     cap = (i2["lds_fixed_bytes"] + i4["lds_fixed_bytes"]) // 2
     old = os.environ.get("RTX_LDS_CAP")

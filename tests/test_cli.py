@@ -121,6 +121,42 @@ def test_cli_render_writes_reference_ppm(tmp_path):
     assert (got != want).mean() < 0.01
 
 
+@pytest.mark.gpu
+def test_cli_ppm_equals_device_quantised_frame(tmp_path):
+    """The PPM the CLI writes is, byte for byte, rt_to_bytes_device of the same
+    GPU frame (same scene, seed, camera and device): write_color's quantiser
+    (ColorUtility.hpp:11-36, StaticCamera.cpp:50-57) on the host equals the
+    library's device quantiser, one device or sharded (--shards 3: rt_multi's
+    device exchange, bit-identical to one device)."""
+    import ctypes as C
+    import numpy as np
+    torch = pytest.importorskip("torch")
+    from rtx.lib import load
+    from rtx.render import Renderer, camera_frame
+    path = os.path.join(PKG, "scenes", "cornell.json")
+    S = load_scene(path)
+    cam = S.camera_desc(image_width=40, samples_per_pixel=16, max_depth=6)
+    f = camera_frame(cam)
+    buf = torch.zeros((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda:0")
+    with Renderer(S) as R:
+        stream = torch.cuda.current_stream().cuda_stream
+        R.render_device(f, buf.data_ptr(), stream, seed=5, output=abi.RT_OUT_SUM)
+        dev = torch.empty(buf.numel(), dtype=torch.uint8, device="cuda:0")
+        assert load().rt_to_bytes_device(C.c_void_p(buf.data_ptr()), buf.numel() // 3,
+                                         f.pixel_samples_scale, C.c_void_p(dev.data_ptr()),
+                                         C.c_void_p(stream)) == 0
+        torch.cuda.synchronize()
+    want = dev.cpu().numpy().astype(np.int64)
+    for extra in ([], ["--shards", "3"]):
+        r = _run("--scene", path, "--width", "40", "--samples", "16", "--depth", "6",
+                 "--seed", "5", "--output", "t.ppm", *extra, cwd=str(tmp_path))
+        assert r.returncode == 0, r.stderr
+        data = (tmp_path / "output" / "t.ppm").read_text().split()
+        assert data[:4] == ["P3", str(f.image_width), str(f.image_height), "255"]
+        got = np.array([int(x) for x in data[4:]], dtype=np.int64)
+        assert np.array_equal(got, want), extra
+
+
 CHECK = os.path.join(PKG, "build", "rtx_scene_check")
 
 
