@@ -609,9 +609,51 @@ RT_HD RT_FI bool quad_t_aa(const DQuad &q, const Ray &r, double tmin, double tma
   t = tt;
   return true;
 }
-template <bool SEL = false>
+// quad_t_aa with the axes (k, i, j) as constants: the ray's components and the
+// record's fields are picked at compile time, not by per-lane selects (four
+// v_cndmask per double component read by an axis held in a register, 24 per
+// test), and the sign `neg` is the permutation's parity.  The same operations
+// on the same values as quad_t_aa, so the same t and the same verdict.
+RT_HD RT_FI constexpr double comp_c(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+template <int K, int I, int J>
+RT_HD RT_FI bool quad_t_aa_c(const DQuad &q, const Ray &r, double tmin, double tmax, double &t) {
+  constexpr bool neg = !((K + 1) % 3 == I); // (k, i, j) not a cyclic shift of (0, 1, 2)
+  const double nk = q.n[K], wk = q.w[K], Qi = q.Q[I], Qj = q.Q[J], vj = q.v[J], ui = q.u[I];
+  const double denom = nk * comp_c(r.d, K);
+  if (fabs(denom) < 1e-8 || fabs(denom) == kInf) return false;
+  const double tt = (q.D - nk * comp_c(r.o, K)) / denom;
+  if (!(tmin <= tt && tt <= tmax)) return false;
+  const double pvi = (comp_c(r.o, I) + tt * comp_c(r.d, I)) - Qi;
+  const double pvj = (comp_c(r.o, J) + tt * comp_c(r.d, J)) - Qj;
+  const double ca = pvi * vj, cb = ui * pvj;
+  const double alpha = wk * (neg ? -ca : ca);
+  const double beta = wk * (neg ? -cb : cb);
+  if (!(0 <= alpha && alpha <= 1) || !(0 <= beta && beta <= 1)) return false;
+  t = tt;
+  return true;
+}
+// Dispatch on a WAVE-UNIFORM aa (the flat list walk, the light loops: one
+// record for every lane): scalar branches to the constant-axis form.  A
+// per-lane aa (BVH leaves) keeps quad_t_aa: a switch would serialise there.
+#ifndef RT_QUAD_AXES
+#define RT_QUAD_AXES 1
+#endif
+RT_HD RT_FI bool quad_t_aa_u(const DQuad &q, const Ray &r, double tmin, double tmax, double &t) {
+  switch (q.aa & 63) {
+  case 0 | 1 << 2 | 2 << 4: return quad_t_aa_c<0, 1, 2>(q, r, tmin, tmax, t);
+  case 0 | 2 << 2 | 1 << 4: return quad_t_aa_c<0, 2, 1>(q, r, tmin, tmax, t);
+  case 1 | 2 << 2 | 0 << 4: return quad_t_aa_c<1, 2, 0>(q, r, tmin, tmax, t);
+  case 1 | 0 << 2 | 2 << 4: return quad_t_aa_c<1, 0, 2>(q, r, tmin, tmax, t);
+  case 2 | 0 << 2 | 1 << 4: return quad_t_aa_c<2, 0, 1>(q, r, tmin, tmax, t);
+  default: return quad_t_aa_c<2, 1, 0>(q, r, tmin, tmax, t);
+  }
+}
+template <bool SEL = false, bool UAX = false> // UAX: q is the same record in every lane
 RT_HD RT_FI bool quad_t(const DQuad &q, const Ray &r, double tmin, double tmax,
                                        double &t) { // Plane.cpp:76-100
+  if constexpr (UAX && RT_QUAD_AXES) {
+    if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa_u(q, r, tmin, tmax, t);
+  }
   if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa<SEL>(q, r, tmin, tmax, t);
   V3 n = ld3(q.n);
   double denom = dot(n, r.d);
@@ -1471,8 +1513,9 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                          tmin, tmax, t, moving, true, yl);
     }
     if (STATS) cnt.quads++;
-    if constexpr (U) return quad_t<true>(ldu<true>(S.quads, it.idx), lr, tmin, tmax, t);
-    return quad_t(S.quads[it.idx], lr, tmin, tmax, t);
+    constexpr bool UA = decltype(uniform)::value; // the flat walk: the same quad in every lane
+    if constexpr (U) return quad_t<true, UA>(ldu<true>(S.quads, it.idx), lr, tmin, tmax, t);
+    return quad_t<false, UA>(S.quads[it.idx], lr, tmin, tmax, t);
   };
   [[maybe_unused]] auto item_root = [&](int ii, const Ray &rr, double ra, double ry, double tmax,
                                         double &t) -> bool {
@@ -1850,7 +1893,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
       if (STATS) cnt.light++;
       const DQuad &q = S.quads[L.idx];
       double t;
-      if (quad_t(q, lr, 0.001, kInf, t)) {
+      if (quad_t<false, true>(q, lr, 0.001, kInf, t)) { // the same light in every lane
         V3 n = ld3(q.n);
         V3 fn = dot(lr.d, n) < 0 ? n : -n;
         double d2 = t * t * len2(lr.d);
