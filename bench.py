@@ -57,6 +57,21 @@ CONFIGS = {
 }
 
 
+def tuning_from_env():
+    """A/B runs only (profiles/ab.sh NAME=VALUE variants): RTX_TUNING =
+    "field=value,..." of rt_tuning fields (rtx.abi.Tuning) for the bench's
+    scenes.  The library itself reads no environment (ABI 4); unset = the
+    default plan."""
+    spec = os.environ.get("RTX_TUNING", "").strip()
+    if not spec:
+        return None
+    out = {}
+    for kv in spec.split(","):
+        k, v = kv.split("=")
+        out[k.strip()] = float(v) if k.strip() == "tail_tiles" else int(v)
+    return out
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -400,7 +415,7 @@ def other_configs(args, torch, dev, skip, pmcs):
         S = load_scene(os.path.join(SCENES, name + ".json"))
         f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
         buf = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
-        with Renderer(S, device=dev.index or 0) as R:
+        with Renderer(S, device=dev.index or 0, tuning=tuning_from_env()) as R:
             def go(seed):
                 R.render_device(f, buf.data_ptr(), 0, seed=seed, output=abi.RT_OUT_SUM, accumulate=0)
             for w in range(warm):
@@ -575,6 +590,8 @@ def main():
                     help="rank 0 compares the reduced frame with a 1-device render")
     ap.add_argument("--pmc-save", default="",
                     help="write the live PMC summary (the pmc_<config>.json format) here")
+    ap.add_argument("--shard-units", type=int, default=0,
+                    help="N>1 tile shards: work units per rank (0: rtx.dist.shard_units)")
     ap.add_argument("--pmc", default="auto", choices=["auto", "file", "off"],
                     help="N=1 roofline counters: auto = rocprofv3 PMC passes of this build "
                          "run before the timed run (fallback: the committed "
@@ -627,7 +644,7 @@ def main():
     tiles_mode = (use_pg and args.shard == "tiles") or (ws == 1 and args.n1_layout == "tiles")
 
     from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks
-    R = Renderer(scene, device=local)
+    R = Renderer(scene, device=local, tuning=tuning_from_env())
     info = R.info()
     stream = torch.cuda.current_stream(dev)  # the null stream: ordered with RCCL's waits
 
@@ -642,7 +659,8 @@ def main():
                         layout=abi.RT_LAYOUT_TILES, chunks=chunks)
 
     if tiles_mode:
-        shard = TileShardedRenderer(tile_render_fn, frame, rank, ws)
+        shard = TileShardedRenderer(tile_render_fn, frame, rank, ws,
+                                    target_units=args.shard_units or None)
         bufs = [shard.buffer(dev) for _ in range(2)]
         gath = [shard.gather_buffer(dev) if rank == 0 else None for _ in range(2)]
         sums = [shard.sum_buffer(dev) for _ in range(2)]   # per-tile sums (device chunk sum)

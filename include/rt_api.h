@@ -13,6 +13,9 @@
  *                        (+ HittableConverter::cpu_to_cuda_hittable, HittableConverter.cuh:50-111,
  *                           MaterialConverter.cuh:26-121, TextureConverter.cuh:19-88,
  *                           CudaSceneContext::initialize/finalize_and_upload, CudaSceneContext.cuh:71-123)
+ *   rt_scene_create_tuned <- the same with the launch / staging / builder tuning passed
+ *                        explicitly (rt_tuning; the reference's CameraConfig,
+ *                        src/core/camera/CameraConfig.hpp:9-62, carries its settings the same way)
  *   rt_scene_destroy  <- cleanup_cuda_scene             src/scene/CudaSceneInitialization.cuh:302-308
  *   rt_render         <- cuda_init_rand_states_wrapper  src/core/camera/CameraKernelWrappers.cuh:11-13
  *                        + cuda_static_render_wrapper   src/core/camera/CameraKernelWrappers.cuh:25-34
@@ -69,7 +72,10 @@ extern "C" {
    2: rt_scene_desc.bvh_arity, rt_path_stats.cyc_*, rt_scene_info's stack and
       LDS fields.
    3: rt_tiles_sum_device, rt_tiles_to_frame_device, rt_multi_gather_ms; the
-      rt_multi exchange runs on the devices. */
+      rt_multi exchange runs on the devices.
+   4: rt_tuning with rt_scene_create_tuned / rt_multi_create_tuned (the
+      library reads no environment variables); rt_path_stats.medium_box_*;
+      rt_scene_info.lds_node_bytes. */
 #define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
@@ -342,7 +348,43 @@ int rt_device_count(int32_t *count);
 
 int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame);
 
+/* Tuning of one scene's launches, passed explicitly at creation instead of
+   read from the process environment (the reference passes its configuration
+   the same way, CameraConfig.hpp:9-62).  A zero-filled struct is the default
+   plan of every field -- what rt_scene_create uses.  None of the fields
+   changes a rendered value: the frame is the same sum of the same samples,
+   only its split into work units, the LDS staging and the BVH builder's
+   parameters move (work-unit splits regroup a pixel's fp64 chunk sums, so
+   frames of different splits agree to rounding, not bit for bit). */
+typedef struct rt_tuning {
+  /* frame work units (rt_render*, rt_multi_render) */
+  int32_t chunk_target;   /* uniform split: work units per wave slot; 0: 32; < 0: whole tiles only */
+  int32_t head_strata;    /* head/tail plan: strata per head unit; 0: 64 up to 64 strata, else 128 */
+  int32_t tail_split;     /* tail chunks per head chunk; 0: 8 */
+  int32_t no_uniform_tail; /* 1: no finer last chunks in the uniform split */
+  int32_t no_persistent;  /* 1: one work unit per wavefront (no persistent unit loop) */
+  int32_t grid_cap;       /* persistent launches: at most this many blocks; 0: every resident one */
+  double tail_tiles;      /* tail tiles per wave slot; 0: 0.5; < 0: no tail plan */
+  /* LDS staging (rt_scene_create) */
+  int32_t lds_nodes;      /* one-unit instances: at most this many BVH nodes; 0: the plan; < 0: none */
+  int32_t lds_nodes_pc;   /* the persistent instance's node prefix, the same rule */
+  int32_t no_lds_prims;   /* 1: the persistent instance stages no items / spheres */
+  int32_t no_lds_perlin;  /* 1: the Perlin table stays in HBM */
+  int32_t lds_cap;        /* per-block LDS cap in bytes; 0: 64 KB (tests of the stack fallback) */
+  int32_t pc_waves;       /* persistent blocks: 0 auto; 4: the 4-wave form on any scene (tests) */
+  /* world BVH builders */
+  int32_t sah_stack_budget; /* device SAH: depth of the balanced-split switch; 0: RT_STACK_DEPTH-2 */
+  int32_t lbvh_max_depth;   /* device trees deeper than this fall back to the host SAH; 0: RT_STACK_DEPTH-1 */
+  int32_t sah_leaf_max, sah_leaf_split; /* host SAH leaf rules; 0: the builder's defaults */
+  int32_t sah_trav_x4, sah_bins;        /* host SAH traversal cost x4, bins; 0: 4, 16 */
+  int32_t extra_features;   /* RT_FEAT_* bits OR'ed into the kernel instance key (debug) */
+  int32_t reserved[7];
+} rt_tuning;
+
 int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **scene);
+/* rt_scene_create with explicit tuning (NULL: the default, as rt_scene_create) */
+int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tuning *tuning,
+                          rt_scene **scene);
 int rt_scene_info_get(const rt_scene *scene, rt_scene_info *info);
 int rt_scene_destroy(rt_scene *scene);
 
@@ -412,6 +454,9 @@ typedef struct rt_multi rt_multi; /* opaque: one rt_scene per shard */
 #define RT_MULTI_MAX_SHARDS 256
 int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
                     int32_t n_shards, rt_multi **multi);
+/* ... every shard's scene created with `tuning` (NULL: the default) */
+int rt_multi_create_tuned(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
+                          int32_t n_shards, const rt_tuning *tuning, rt_multi **multi);
 
 /* rt_render over the shards: shard k renders the 8x8 tiles t = k (mod
    n_shards) of the row range, all launched strata, in (tile, stratum chunk)

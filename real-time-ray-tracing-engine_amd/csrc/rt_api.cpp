@@ -26,8 +26,9 @@
 extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const DLaunch *P,
                                         double *out, unsigned long long *stats,
                                         hipStream_t stream);
-extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan);
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes,
+extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, int lds_cap, RtkLdsPlan *plan);
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int force_waves, int *pcw,
+                                      int64_t *free_bytes,
                                       int *blocks_per_cu);
 extern "C" int rtk_lds_prims_enabled(void);
 extern "C" int rtk_lds_perlin_enabled(void);
@@ -73,6 +74,7 @@ struct rt_scene {
   int wave_slots = 0;        // resident waves of the render instance on this device
   int pc_grid = 0;           // resident blocks of the persistent instance on this device
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
+  rt_tuning tune{};          // explicit tuning (rt_scene_create_tuned; zero: the default plan)
 };
 
 namespace {
@@ -222,10 +224,10 @@ int rt_camera_setup(const rt_camera_desc *camera, rt_frame *frame) {
 // scene order at `items`): the binned-SAH builder (rt_bvh_sah.hip) or the linear
 // BVH (rt_bvh_build.hip); writes the nodes and the items in leaf order in place.
 // Depth at which the device SAH builder switches to balanced splits (the host
-// builder's force_median bound); RTX_SAH_STACK_BUDGET lowers it in tests.
-static int sah_stack_budget() {
+// builder's force_median bound); rt_tuning.sah_stack_budget lowers it in tests.
+static int sah_stack_budget(const rt_tuning &t) {
   int b = RT_STACK_DEPTH - 2;
-  if (const char *v = std::getenv("RTX_SAH_STACK_BUDGET")) b = std::max(1, std::min(b, std::atoi(v)));
+  if (t.sah_stack_budget > 0) b = std::max(1, std::min(b, (int)t.sah_stack_budget));
   return b;
 }
 struct DeviceTree {
@@ -250,7 +252,7 @@ static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *
                      s->stream);
   if (sah) {
     if (e == hipSuccess)
-      e = rtk_build_sah(d_box, items, n, nodes, d_sorted, d_lb, lb, sah_stack_budget(),
+      e = rtk_build_sah(d_box, items, n, nodes, d_sorted, d_lb, lb, sah_stack_budget(s->tune),
                         &tree.n_nodes, &tree.depth, &tree.root_leaf, s->stream);
   } else {
     tree.n_nodes = n - 1;
@@ -268,9 +270,20 @@ static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *
 }
 
 int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
+  return rt_scene_create_tuned(desc, device, nullptr, out);
+}
+
+int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tuning *tuning,
+                          rt_scene **out) {
   if (!out) return set_err(RT_ERR_INVALID, "null output pointer");
   *out = nullptr;
+  rt_tuning tune{};
+  if (tuning) tune = *tuning;
   rtx::HostScene H;
+  H.sah_leaf_max = tune.sah_leaf_max;
+  H.sah_leaf_split = tune.sah_leaf_split;
+  H.sah_trav_x4 = tune.sah_trav_x4;
+  H.sah_bins = tune.sah_bins;
   std::string err;
   int rc = rtx::compile_scene(desc, H, err);
   if (rc != RT_OK) return set_err(rc, err);
@@ -323,6 +336,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
 
   rt_scene *s = new rt_scene();
   s->device = device;
+  s->tune = tune;
   s->block_bytes = off;
   e = hipMalloc((void **)&s->block, off);
   if (e != hipSuccess) {
@@ -355,7 +369,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     if (!want4 || H.root_is_leaf || H.nodes.empty()) return hipSuccess;
     const int d4 = rtx::collapse_bvh4(H.nodes, H.nodes4);
     RtkLdsPlan plan4{};
-    hipError_t fe = rtk_lds_plan(features | RT_FEAT_BVH4, rtx::bvh4_stack_depth(d4), &plan4);
+    hipError_t fe = rtk_lds_plan(features | RT_FEAT_BVH4, rtx::bvh4_stack_depth(d4), tune.lds_cap, &plan4);
     if (fe != hipSuccess) return fe;
     if (rtx::bvh4_stack_depth(d4) > RT_STACK_DEPTH4 || !plan4.stack_fits) {
       H.nodes4.clear();
@@ -398,8 +412,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   if (!H.lights.empty()) d.features |= RT_FEAT_LIGHTS;
   for (const DTex &t : H.texs)
     if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
-  if (const char *fx = std::getenv("RTX_EXTRA_FEATURES")) // debug: widen the instance
-    d.features |= std::atoi(fx) & 15;
+  d.features |= tune.extra_features & 15; // debug: widen the instance
   // device-built world BVH (rt_bvh_build.hip), host SAH fallback if the linear
   // tree is deeper than the traversal stack
   int builder = RT_BVH_HOST;
@@ -410,8 +423,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       rt_scene_destroy(s);
       return hip_err(be, "device BVH build");
     }
-    int max_depth = RT_STACK_DEPTH - 1;
-    if (const char *md = std::getenv("RTX_LBVH_MAX_DEPTH")) max_depth = std::atoi(md); // tests
+    const int max_depth = tune.lbvh_max_depth > 0 ? (int)tune.lbvh_max_depth : RT_STACK_DEPTH - 1;
     if (tree.depth >= 0 && tree.depth <= max_depth) {
       H.bvh_depth = tree.depth;
       H.nodes.resize(tree.n_nodes); // the device arrays hold the tree; sizes only
@@ -467,7 +479,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
   RtkLdsPlan plan{};
   {
     int cus = 0;
-    hipError_t be = rtk_lds_plan(d.features, d.stack_depth, &plan);
+    hipError_t be = rtk_lds_plan(d.features, d.stack_depth, tune.lds_cap, &plan);
     if (be == hipSuccess) be = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (be != hipSuccess) {
       rt_scene_destroy(s);
@@ -491,8 +503,8 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
       budget = 0;
       s->wave_slots = cus * plan.resident_waves_per_cu;
     }
-    if (const char *ln = std::getenv("RTX_LDS_NODES")) // A/B experiments, within the plan
-      budget = std::min(std::atoi(ln), plan.n_nodes);
+    if (tune.lds_nodes != 0) // A/B experiments, within the plan (< 0: none)
+      budget = std::max(0, std::min((int)tune.lds_nodes, plan.n_nodes));
     d.n_lds_nodes = std::max(0, std::min(budget, d.n_nodes));
     // the persistent instance: its node prefix, then -- if the whole tree is
     // staged and room is left -- the world items and spheres (-1: no
@@ -500,7 +512,7 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     int64_t pc_free = -1;
     int pcw = 0;
     int pc_bpc = 0;
-    be = rtk_lds_plan_pc(d.features, d.stack_depth, &pcw, &pc_free, &pc_bpc);
+    be = rtk_lds_plan_pc(d.features, d.stack_depth, tune.pc_waves, &pcw, &pc_free, &pc_bpc);
     d.pc_waves = pcw;
     s->pc_grid = cus * pc_bpc;
     if (be != hipSuccess) {
@@ -509,26 +521,22 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **out) {
     }
     const int64_t node_b = RT_LDS_NODE_BYTES(d.features);
     d.n_lds_nodes_pc = pc_free < 0 ? -1 : (int32_t)std::min<int64_t>(pc_free / node_b, d.n_nodes);
-    if (const char *ln = std::getenv("RTX_LDS_NODES_PC")) // A/B experiments
-      if (d.n_lds_nodes_pc >= 0) // within what the plan leaves free
-        d.n_lds_nodes_pc = (int32_t)std::min<int64_t>({(int64_t)std::atoi(ln), d.n_nodes, pc_free / node_b});
+    if (tune.lds_nodes_pc != 0 && d.n_lds_nodes_pc >= 0) // A/B experiments, within what the plan leaves free
+      d.n_lds_nodes_pc = (int32_t)std::max<int64_t>(
+          0, std::min<int64_t>({(int64_t)tune.lds_nodes_pc, d.n_nodes, pc_free / node_b}));
     d.lds_items_pc = d.lds_spheres_pc = 0;
     const int64_t prim_b = (int64_t)(H.items.size() * sizeof(DItem) + H.spheres.size() * sizeof(DSphere));
-    const char *lp_env = std::getenv("RTX_LDS_PRIMS"); // 0: A/B experiments
-    if (rtk_lds_prims_enabled() && !(lp_env && lp_env[0] == '0') && pc_free >= 0 &&
+    if (rtk_lds_prims_enabled() && !tune.no_lds_prims && pc_free >= 0 &&
         d.n_lds_nodes_pc == d.n_nodes && pc_free - (int64_t)d.n_nodes * node_b >= prim_b &&
         !H.items.empty()) {
       d.lds_items_pc = (int32_t)H.items.size();
       d.lds_spheres_pc = (int32_t)H.spheres.size();
     }
   }
-  // the one Perlin table of a noise scene in LDS (RTX_LDS_PERLIN=0: from HBM,
-  // A/B runs and the bit-identity test); several tables stay in HBM
-  {
-    const char *pe = std::getenv("RTX_LDS_PERLIN");
-    d.lds_perlin = (d.features & RT_FEAT_NOISE) && H.perlin.size() == 1 && rtk_lds_perlin_enabled() &&
-                   !(pe && pe[0] == '0');
-  }
+  // the one Perlin table of a noise scene in LDS (tune.no_lds_perlin: from
+  // HBM, A/B runs and the bit-identity test); several tables stay in HBM
+  d.lds_perlin = (d.features & RT_FEAT_NOISE) && H.perlin.size() == 1 && rtk_lds_perlin_enabled() &&
+                 !tune.no_lds_perlin;
   s->stats = (unsigned long long *)(s->block + parts[iSt].off);
   s->unit_ctr = (int32_t *)(s->block + parts[iUc].off);
 
@@ -598,7 +606,7 @@ int rt_scene_destroy(rt_scene *s) {
 //    same as 64 with half the partial writes (r04b).
 //  * Otherwise every tile split, ~RTX_CHUNK_TARGET (default 32) units per
 //    wave slot (the round-1 rule), the last tiles again in finer chunks.
-// RTX_CHUNK_TARGET=0: whole tiles only (tests).
+// rt_tuning.chunk_target < 0: whole tiles only (tests).
 struct SplitPlan {
   int n_head, head_chunks, chunks; // head tiles, their chunks; the tail tiles' chunks
 };
@@ -609,8 +617,8 @@ static size_t plan_parts(const SplitPlan &sp, int n_local) { // chunk partial re
 static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   SplitPlan sp{L.n_local_tiles, 1, 1};
   if (L.compact || L.tile_stride != 1 || L.tile_first != 0 || L.sample_count < 2) return sp;
-  int target = 32;
-  if (const char *t = std::getenv("RTX_CHUNK_TARGET")) target = std::atoi(t);
+  const rt_tuning &tu = s->tune;
+  const int target = tu.chunk_target == 0 ? 32 : tu.chunk_target;
   if (target <= 0 || s->wave_slots <= 0) return sp;
   // wave slots of the instance that runs the launch (the persistent one's own
   // residency for the feature sets that have one)
@@ -621,16 +629,13 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
     const int64_t cs = (L.sample_count + c - 1) / c;
     return (int)((L.sample_count + cs - 1) / cs);
   };
-  double tail = 0.5;
-  if (const char *t = std::getenv("RTX_TAIL_TILES")) tail = std::atof(t);
+  const double tail = tu.tail_tiles == 0.0 ? 0.5 : std::max(0.0, tu.tail_tiles);
   // head units: whole tiles up to 64 strata (C2); beyond, chunks of 128
   // strata (C3: 2 per tile -- as fast as 4 chunks of 64, half the partial
   // writes; whole 256-strata tiles -9 %, profiles/r04b_head_strata_ab.log)
-  int head_max = L.sample_count <= 64 ? 64 : 128;
-  if (const char *h = std::getenv("RTX_HEAD_STRATA")) head_max = std::max(1, std::atoi(h));
+  const int head_max = tu.head_strata > 0 ? (int)tu.head_strata : L.sample_count <= 64 ? 64 : 128;
   const int64_t head_chunks = (L.sample_count + head_max - 1) / head_max;
-  int split = 8; // tail chunks per head chunk (RTX_TAIL_SPLIT: A/B runs)
-  if (const char *t = std::getenv("RTX_TAIL_SPLIT")) split = std::max(1, std::atoi(t));
+  const int split = tu.tail_split > 0 ? (int)tu.tail_split : 8; // tail chunks per head chunk
   // partial records of a head/tail plan: bounded by 4 frames (a tail of
   // chunked tiles + head chunks); otherwise the uniform split
   const bool bounded = head_chunks == 1 || head_chunks * tiles <= 4 * tiles;
@@ -648,9 +653,8 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   // ... with the last `slots` x RTX_TAIL_TILES tiles in `split` times finer
   // chunks when the frame has a tile per wave slot (C4, C5: the uniform
   // units last 15 / 84 ms: C4 +1.7 %, C5 +0.9 %, profiles/r03ae_ab.log;
-  // RTX_UNIFORM_TAIL=0: off, A/B runs)
-  const char *ut = std::getenv("RTX_UNIFORM_TAIL");
-  if (!(ut && ut[0] == '0') && sp.chunks > 1 && tiles > slots && tail > 0) {
+  // rt_tuning.no_uniform_tail: off, A/B runs)
+  if (!tu.no_uniform_tail && sp.chunks > 1 && tiles > slots && tail > 0) {
     const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
     const int tc = no_empty(split * (int64_t)sp.chunks);
     if (tc > sp.chunks && n_tail < tiles) {
@@ -688,20 +692,16 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
     int rc = ensure_scratch(s, std::max<size_t>(1, n_parts * 64 * 3) * sizeof(double));
     if (rc) return rc;
   }
-  // persistent waves pulling work units (RT_PERSISTENT=0 in the environment:
-  // one unit per wave, for A/B runs)
-  static const bool persistent = [] {
-    const char *v = getenv("RT_PERSISTENT");
-    return !(v && v[0] == '0');
-  }();
+  // persistent waves pulling work units (rt_tuning.no_persistent: one unit
+  // per wave, for A/B runs)
+  const bool persistent = !s->tune.no_persistent;
   DLaunch Lp = L;
   if (persistent && s->wave_slots > 0) {
     Lp.unit_ctr = s->unit_ctr;
     Lp.grid_cap = s->pc_grid > 0 ? s->pc_grid // resident persistent blocks
                                  : std::max(1, s->wave_slots / std::max(1, s->ds.pc_waves));
-    // RT_GRID_CAP: fewer resident blocks (tests: many units per wave)
-    if (const char *g = getenv("RT_GRID_CAP"))
-      if (atoi(g) > 0) Lp.grid_cap = atoi(g);
+    // rt_tuning.grid_cap: fewer resident blocks (tests: many units per wave)
+    if (s->tune.grid_cap > 0) Lp.grid_cap = s->tune.grid_cap;
   }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
@@ -926,6 +926,11 @@ int rt_multi_destroy(rt_multi *m) {
 
 int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
                     int32_t n_shards, rt_multi **out) {
+  return rt_multi_create_tuned(desc, devices, n_devices, n_shards, nullptr, out);
+}
+
+int rt_multi_create_tuned(const rt_scene_desc *desc, const int32_t *devices, int32_t n_devices,
+                          int32_t n_shards, const rt_tuning *tuning, rt_multi **out) {
   if (!out || !desc || !devices) return set_err(RT_ERR_INVALID, "null argument");
   *out = nullptr;
   if (n_devices < 1 || n_shards < n_devices)
@@ -943,7 +948,7 @@ int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices, int32_t n
     try {
       for (int k = 0; k < n_shards; ++k)
         th.emplace_back([&, k]() {
-          rc[k] = rt_scene_create(desc, devices[k % n_devices], &m->scenes[k]);
+          rc[k] = rt_scene_create_tuned(desc, devices[k % n_devices], tuning, &m->scenes[k]);
           if (rc[k] != RT_OK) err[k] = g_err; // thread-local message of this worker
         });
     } catch (const std::exception &ex) { // thread creation failed: join the started ones

@@ -623,9 +623,9 @@ static size_t lds_bytes_pc(int features, int pcw, int stack_depth, int n_lds_nod
 // LDS plan per block at the occupancy the instance's register count allows
 // (blocks of kWaves waves over the 4 SIMDs): the bytes left for the staged BVH
 // prefix after the static LDS and the traversal stacks, and whether those two
-// fit at all (the caller then keeps a shallower tree).  RTX_LDS_CAP lowers the
-// per-block cap (tests of that fallback).
-extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *plan) {
+// fit at all (the caller then keeps a shallower tree).  lds_cap > 0 lowers the
+// per-block cap (rt_tuning.lds_cap: tests of that fallback).
+extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, int lds_cap, RtkLdsPlan *plan) {
   hipFuncAttributes a;
   hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(render_table(false)[features & F_ALL]));
   if (e != hipSuccess) return e;
@@ -634,8 +634,7 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
   if (waves_per_simd > 8) waves_per_simd = 8;
   if (waves_per_simd < 1) waves_per_simd = 1;
   size_t lds_cu = 160 * 1024, cap = 64 * 1024; // per CU; per block without opt-in
-  if (const char *c = getenv("RTX_LDS_CAP"))
-    if (atoi(c) > 0 && (size_t)atoi(c) < cap) cap = (size_t)atoi(c);
+  if (lds_cap > 0 && (size_t)lds_cap < cap) cap = (size_t)lds_cap;
   const int bw = block_waves((unsigned)features);
   const int blocks_per_cu = waves_per_simd * 4 / bw > 0 ? waves_per_simd * 4 / bw : 1;
   size_t per_block = lds_cu / blocks_per_cu;
@@ -659,16 +658,16 @@ extern "C" hipError_t rtk_lds_plan(int features, int stack_depth, RtkLdsPlan *pl
 // (one per SIMD at the occupancy target: a quarter of the CU's LDS each);
 // *pcw = 0 / *free_bytes = -1 when neither fits or the feature set has no
 // persistent instance.
-extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int *pcw, int64_t *free_bytes,
+extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int force_waves, int *pcw,
+                                      int64_t *free_bytes,
                                       int *blocks_per_cu) {
   *free_bytes = -1;
   *pcw = 0;
   *blocks_per_cu = 0;
   const unsigned f = (unsigned)(features & F_ALL);
   if (!RT_PERSIST_F(f)) return hipSuccess;
-  const char *force = getenv("RTX_PC_WAVES"); // tests: the 4-wave form on any scene
-  for (int w : {kPcWaves, kWaves}) {
-    if (force && atoi(force) == kWaves && w != kWaves) continue;
+  for (int w : {kPcWaves, kWaves}) { // force_waves == kWaves (tests): the 4-wave form on any scene
+    if (force_waves == kWaves && w != kWaves) continue;
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(persistent_instance(f, w)));
     if (e != hipSuccess) return e;

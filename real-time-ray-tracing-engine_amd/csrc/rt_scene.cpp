@@ -27,10 +27,7 @@
 namespace rtx {
 namespace {
 
-int env_int(const char *name, int dflt) {
-  const char *v = std::getenv(name);
-  return v && *v ? std::atoi(v) : dflt;
-}
+int or_default(int32_t v, int dflt) { return v > 0 ? v : dflt; }
 
 const double kInf = std::numeric_limits<double>::infinity();
 const double kPi = 3.1415926535897932385;
@@ -123,18 +120,19 @@ struct SahBuilder {
   // use single-item leaves: the wave tests leaves together, so a lane's
   // second leaf item costs the whole wave a trip (C3: 2 / 4 -> 1 / 1 gave
   // +2.1 %, profiles/r02aj_sah_leaf_sweep.log); the 4-wide and device-built
-  // trees keep 2 / 4 (the device SAH builder's rules).  Measurement overrides:
-  // RT_SAH_LEAF_MAX, RT_SAH_LEAF_SPLIT, RT_SAH_TRAV_X4 (4 x trav_cost).
+  // trees keep 2 / 4 (the device SAH builder's rules).  Measurement overrides
+  // (rt_tuning, via HostScene): sah_leaf_max, sah_leaf_split, sah_trav_x4 (4 x
+  // trav_cost), sah_bins.
   int leaf_max = 2, leaf_split = 4;
   double trav_cost = 1.0;
   static constexpr int kMaxBins = 64;
-  int sah_bins = 16; // centroid bins per axis (RT_SAH_BINS: measurement override, <= 64)
+  int sah_bins = 16; // centroid bins per axis (sah_bins override, <= 64)
   void set_leaf_rules(size_t n_items) {
     const bool binary = n_items < (size_t)kBvh4Min;
-    leaf_max = env_int("RT_SAH_LEAF_MAX", binary ? 1 : 2);
-    leaf_split = env_int("RT_SAH_LEAF_SPLIT", binary ? 1 : 4);
-    trav_cost = env_int("RT_SAH_TRAV_X4", 4) / 4.0;
-    sah_bins = std::min(kMaxBins, std::max(2, env_int("RT_SAH_BINS", 16)));
+    leaf_max = or_default(H.sah_leaf_max, binary ? 1 : 2);
+    leaf_split = or_default(H.sah_leaf_split, binary ? 1 : 4);
+    trav_cost = or_default(H.sah_trav_x4, 4) / 4.0;
+    sah_bins = std::min(kMaxBins, std::max(2, or_default(H.sah_bins, 16)));
   }
 
   int build(std::vector<BRef> &r, int st, int en, int dep) {

@@ -34,6 +34,9 @@ struct HostScene {
   // in scene order, their boxes (lo xyz, hi xyz) and the centroid bounds; nodes
   // sized, not filled
   int32_t device_bvh = 0;
+  // host SAH builder overrides (rt_tuning sah_*; 0: the builder's defaults),
+  // set by the caller before compile_scene
+  int32_t sah_leaf_max = 0, sah_leaf_split = 0, sah_trav_x4 = 0, sah_bins = 0;
   std::vector<double> item_boxes;
   double scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
 };

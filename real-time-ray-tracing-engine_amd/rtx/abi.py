@@ -124,6 +124,34 @@ class SceneInfo(C.Structure):
                 ("lds_node_bytes", C.c_int32)]
 
 
+class Tuning(C.Structure):
+    """rt_tuning: a scene's work-unit plan, LDS staging and BVH-builder
+    overrides, passed at creation (zero-filled = the default plan)."""
+    _fields_ = [("chunk_target", C.c_int32), ("head_strata", C.c_int32),
+                ("tail_split", C.c_int32), ("no_uniform_tail", C.c_int32),
+                ("no_persistent", C.c_int32), ("grid_cap", C.c_int32),
+                ("tail_tiles", C.c_double),
+                ("lds_nodes", C.c_int32), ("lds_nodes_pc", C.c_int32),
+                ("no_lds_prims", C.c_int32), ("no_lds_perlin", C.c_int32),
+                ("lds_cap", C.c_int32), ("pc_waves", C.c_int32),
+                ("sah_stack_budget", C.c_int32), ("lbvh_max_depth", C.c_int32),
+                ("sah_leaf_max", C.c_int32), ("sah_leaf_split", C.c_int32),
+                ("sah_trav_x4", C.c_int32), ("sah_bins", C.c_int32),
+                ("extra_features", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+
+def tuning(t=None):
+    """A Tuning from None (the default), a Tuning, or a dict of its fields."""
+    if t is None or isinstance(t, Tuning):
+        return t
+    out = Tuning()
+    for k, v in dict(t).items():
+        if k not in dict(Tuning._fields_):
+            raise KeyError("unknown rt_tuning field %r" % k)
+        setattr(out, k, v)
+    return out
+
+
 # Every symbol include/rt_api.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_camera_setup",
@@ -131,4 +159,5 @@ EXPORTS = (
     "rt_render_device", "rt_render_stats", "rt_last_kernel_ms", "rt_to_bytes_device",
     "rt_multi_create", "rt_multi_render", "rt_multi_shard_ms", "rt_multi_destroy",
     "rt_scene_bvh_cost", "rt_tiles_sum_device", "rt_tiles_to_frame_device", "rt_multi_gather_ms",
+    "rt_scene_create_tuned", "rt_multi_create_tuned",
 )

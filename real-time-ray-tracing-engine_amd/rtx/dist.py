@@ -125,10 +125,8 @@ def shard_units(strata):
     per pixel, growing with sqrt(strata / 64) up to 4x -- the fastest of the
     8-way sweeps on one GPU (profiles/r04q_shard_units_*.log,
     r04v_shard_units_*.log): C2 (64 strata) 32768, C3 (256) 65536, C4 (1024)
-    and C5 (4096) 131072; RTX_SHARD_UNITS overrides."""
-    env = os.environ.get("RTX_SHARD_UNITS")
-    if env:
-        return int(env)
+    and C5 (4096) 131072.  A caller overrides it through auto_chunks'
+    target_units (bench.py --shard-units)."""
     return int(32768 * min(4.0, max(1.0, (strata / 64.0) ** 0.5)))
 
 
@@ -159,12 +157,12 @@ class TileShardedRenderer:
     their host tensors."""
 
     def __init__(self, render_fn, frame, rank=0, world=1, chunks=None, tiles_sum=None,
-                 to_frame=None):
+                 to_frame=None, target_units=None):
         self.render_fn = render_fn
         self.frame = frame
         self.rank, self.world = rank, world
         self.n_tiles, self.tiles_per_rank = tile_counts(frame, world)
-        self.chunks = auto_chunks(frame, world) if chunks is None else max(1, chunks)
+        self.chunks = auto_chunks(frame, world, target_units) if chunks is None else max(1, chunks)
         self.tiles_sum = tiles_sum or device_tiles_sum
         self.to_frame = to_frame or device_tiles_to_frame
 

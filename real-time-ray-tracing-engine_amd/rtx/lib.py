@@ -41,6 +41,7 @@ def load():
     L.rt_device_count.argtypes = [P(C.c_int32)]
     L.rt_camera_setup.argtypes = [P(abi.CameraDesc), P(abi.Frame)]
     L.rt_scene_create.argtypes = [P(abi.SceneDesc), C.c_int32, P(C.c_void_p)]
+    L.rt_scene_create_tuned.argtypes = [P(abi.SceneDesc), C.c_int32, P(abi.Tuning), P(C.c_void_p)]
     L.rt_scene_info_get.argtypes = [C.c_void_p, P(abi.SceneInfo)]
     L.rt_scene_destroy.argtypes = [C.c_void_p]
     L.rt_render.argtypes = [C.c_void_p, P(abi.Frame), P(abi.RenderParams), P(C.c_double)]
@@ -51,6 +52,8 @@ def load():
     L.rt_to_bytes_device.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_void_p, C.c_void_p]
     L.rt_multi_create.argtypes = [P(abi.SceneDesc), P(C.c_int32), C.c_int32, C.c_int32,
                                   P(C.c_void_p)]
+    L.rt_multi_create_tuned.argtypes = [P(abi.SceneDesc), P(C.c_int32), C.c_int32, C.c_int32,
+                                        P(abi.Tuning), P(C.c_void_p)]
     L.rt_multi_render.argtypes = [C.c_void_p, P(abi.Frame), P(abi.RenderParams), P(C.c_double)]
     L.rt_multi_shard_ms.argtypes = [C.c_void_p, P(C.c_double)]
     L.rt_multi_destroy.argtypes = [C.c_void_p]

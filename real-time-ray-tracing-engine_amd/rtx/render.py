@@ -23,14 +23,17 @@ def camera_frame(cam):
 
 
 class Renderer:
-    """Owns one device-side scene (rt_scene) on one GPU."""
+    """Owns one device-side scene (rt_scene) on one GPU.  `tuning`: None (the
+    default plan), an abi.Tuning or a dict of its fields (rt_scene_create_tuned)."""
 
-    def __init__(self, scene, device=0):
+    def __init__(self, scene, device=0, tuning=None):
         self.lib = load()
         self.scene_desc = scene
         self._desc = scene.desc()
+        self._tuning = abi.tuning(tuning)
         h = C.c_void_p()
-        check(self.lib.rt_scene_create(C.byref(self._desc), int(device), C.byref(h)))
+        t = C.byref(self._tuning) if self._tuning is not None else None
+        check(self.lib.rt_scene_create_tuned(C.byref(self._desc), int(device), t, C.byref(h)))
         self.handle = h
         self.device = device
 
@@ -141,14 +144,16 @@ class MultiRenderer:
     one host thread per shard, 8x8 tiles dealt round-robin; the multi-device
     form of StaticCamera::render_gpu (StaticCamera.cpp:136-313)."""
 
-    def __init__(self, scene, devices=(0,), shards=None):
+    def __init__(self, scene, devices=(0,), shards=None, tuning=None):
         self.lib = load()
         self._desc = scene.desc()
+        self._tuning = abi.tuning(tuning)
         devs = (C.c_int32 * len(devices))(*devices)
         self.n_shards = int(shards or len(devices))
         h = C.c_void_p()
-        check(self.lib.rt_multi_create(C.byref(self._desc), devs, len(devices), self.n_shards,
-                                       C.byref(h)))
+        t = C.byref(self._tuning) if self._tuning is not None else None
+        check(self.lib.rt_multi_create_tuned(C.byref(self._desc), devs, len(devices),
+                                             self.n_shards, t, C.byref(h)))
         self.handle = h
 
     def close(self):

@@ -86,17 +86,15 @@ def test_c5_full_frame_properties():
                         output=abi.RT_OUT_SUM, accumulate=0)
         torch.cuda.synchronize()
         assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
-        # one work unit per tile (no stratum chunks, no scratch buffer)
-        os.environ["RTX_CHUNK_TARGET"] = "0"
-        try:
-            R.render_device(f, part.data_ptr(), 0, seed=17, output=abi.RT_OUT_SUM, accumulate=0)
-            torch.cuda.synchronize()
-        finally:
-            del os.environ["RTX_CHUNK_TARGET"]
-        assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
         # counters over the whole 4K frame (spp 16 keeps the STATS instance short)
         cam16 = S.camera_desc(image_width=W, samples_per_pixel=16, max_depth=DEPTH)
         st = R.stats(camera_frame(cam16), seed=17)
+    # one work unit per tile (no stratum chunks, no scratch buffer): the split
+    # is chosen through the ABI (rt_tuning.chunk_target < 0), not the environment
+    with Renderer(S, tuning={"chunk_target": -1}) as R:
+        R.render_device(f, part.data_ptr(), 0, seed=17, output=abi.RT_OUT_SUM, accumulate=0)
+        torch.cuda.synchronize()
+    assert torch.allclose(part, full, rtol=1e-11, atol=1e-9)
     assert st["samples"] == W * H * 16
     assert st["samples"] <= st["segments"] <= DEPTH * st["samples"]
     assert 0 < st["shade_events"] <= st["segments"]

@@ -74,12 +74,11 @@ def test_auto_builder_uses_device_for_large_scenes():
     assert np.nanmean(dev) > 0
 
 
-def test_too_deep_device_tree_falls_back_to_host(monkeypatch):
-    monkeypatch.setenv("RTX_LBVH_MAX_DEPTH", "1")
+def test_too_deep_device_tree_falls_back_to_host():
     S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
     S.bvh_builder = abi.RT_BVH_DEVICE
     cam = S.camera_desc(image_width=32, samples_per_pixel=4, max_depth=8)
-    with Renderer(S) as R:
+    with Renderer(S, tuning={"lbvh_max_depth": 1}) as R:
         assert R.info()["bvh_builder"] == abi.RT_BVH_HOST
         img = R.render(camera_frame(cam), seed=9)
     compare(img, O.oracle_render(S, cam, O.MODE_COUNTER, 9), 1e-4)
@@ -107,21 +106,19 @@ def test_device_sah_tree_quality_and_images():
         compare(img[b], img[abi.RT_BVH_HOST], 1e-12)
 
 
-def test_device_sah_depth_budget_balanced_splits(monkeypatch):
+def test_device_sah_depth_budget_balanced_splits():
     """With the stack budget lowered to 8 levels, the device SAH builder switches
     to balanced (count-median) splits below it: the tree stays shallow and the
     image is unchanged."""
-    monkeypatch.setenv("RTX_SAH_STACK_BUDGET", "8")
     S = load_scene(random_spheres(20000, seed=5))
     S.bvh_builder = abi.RT_BVH_DEVICE_SAH
     cam = S.camera_desc(image_width=48, samples_per_pixel=4, max_depth=6)
     f = camera_frame(cam)
-    with Renderer(S) as R:
+    with Renderer(S, tuning={"sah_stack_budget": 8}) as R:
         info = R.info()
         assert info["bvh_builder"] == abi.RT_BVH_DEVICE_SAH
         assert info["bvh_depth"] <= 20, info  # ~log2(20000 / 2) = 14 for exact halves
         dev = R.render(f, seed=6)
-    monkeypatch.delenv("RTX_SAH_STACK_BUDGET")
     S.bvh_builder = abi.RT_BVH_HOST
     with Renderer(S) as R:
         host = R.render(f, seed=6)

@@ -136,13 +136,12 @@ def test_tiles_to_frame_reorders_ragged_frames():
         assert np.array_equal(got, img)
 
 
-def test_shard_chunks_follow_the_strata(monkeypatch):
+def test_shard_chunks_follow_the_strata():
     """8-way tile shards: the work-unit target grows with the strata per pixel
     (profiles/r04q_shard_units_*.log, r04v_shard_units_*.log) and the chunk
-    count leaves no empty chunk; RTX_SHARD_UNITS overrides."""
+    count leaves no empty chunk; an explicit target overrides."""
     from rtx.dist import auto_chunks, shard_units
     from rtx.render import camera_frame
-    monkeypatch.delenv("RTX_SHARD_UNITS", raising=False)
     assert [shard_units(s) for s in (16, 64, 256, 1024, 4096)] == [32768, 32768, 65536, 131072, 131072]
     S = load_scene(SCENE)
     for spp, want in ((64, 8), (256, 16), (1024, 32)):  # C2 / C3 / C4 at 1080p, 8 ranks
@@ -151,8 +150,8 @@ def test_shard_chunks_follow_the_strata(monkeypatch):
         strata = f.sqrt_spp ** 2
         cs = -(-strata // c)
         assert c == want and (c - 1) * cs < strata
-    monkeypatch.setenv("RTX_SHARD_UNITS", "4096")
-    assert shard_units(256) == 4096
+    f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=256, max_depth=8))
+    assert auto_chunks(f, 8, 4096) == 2  # 4,050 tiles per rank: 2 chunks reach 4096 units
 
 
 def _tile_worker(rank, world, port, out_path):
@@ -202,12 +201,9 @@ def test_gpu_tile_layout_reassembles_bit_exact():
     S = load_scene(SCENE)
     cam = S.camera_desc(image_width=44, samples_per_pixel=9, max_depth=6)  # ragged: 44 = 5.5 tiles
     f = camera_frame(cam)
+    with Renderer(S, tuning={"chunk_target": -1}) as R:  # one work unit per tile: same sums bit for bit
+        full = R.render(f, seed=6, output=abi.RT_OUT_SUM)
     with Renderer(S) as R:
-        os.environ["RTX_CHUNK_TARGET"] = "0"  # one work unit per tile: same sums bit for bit
-        try:
-            full = R.render(f, seed=6, output=abi.RT_OUT_SUM)
-        finally:
-            del os.environ["RTX_CHUNK_TARGET"]
         chunked = R.render(f, seed=6, output=abi.RT_OUT_SUM)  # library's auto chunking
         np.testing.assert_allclose(chunked, full, rtol=1e-12, atol=1e-13)
         world = 3

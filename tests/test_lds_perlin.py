@@ -1,7 +1,7 @@
 """The noise instances' LDS copy of the scene's Perlin table
 (rt_path.h perlin_lds, staged once per block in rt_kernel.hip): the fog
 scene's frame must be bit-identical with the table read from HBM
-(RTX_LDS_PERLIN=0 at scene creation: the same arithmetic, only the load
+(rt_tuning.no_lds_perlin at scene creation: the same arithmetic, only the load
 source differs) and match the oracle.  Reference: NoiseTexture.cpp:29-30,
 PerlinNoise.hpp:43-60 (turb over 7 octaves)."""
 import os
@@ -19,16 +19,8 @@ SCENES = os.path.join(O.ROOT, "real-time-ray-tracing-engine_amd", "scenes")
 
 
 def _render(S, f, seed, rows, lds):
-    old = os.environ.get("RTX_LDS_PERLIN")
-    os.environ["RTX_LDS_PERLIN"] = "1" if lds else "0"
-    try:
-        with Renderer(S) as R:
-            return R.info(), R.render(f, seed=seed, rows=rows)
-    finally:
-        if old is None:
-            os.environ.pop("RTX_LDS_PERLIN", None)
-        else:
-            os.environ["RTX_LDS_PERLIN"] = old
+    with Renderer(S, tuning={"no_lds_perlin": 0 if lds else 1}) as R:
+        return R.info(), R.render(f, seed=seed, rows=rows)
 
 
 @pytest.mark.parametrize("width,spp", [(64, 64), (1920, 16)])

@@ -111,7 +111,7 @@ def test_cli_gpus_shards_ppm_byte_identical(tmp_path):
 # (rt_api.cpp frame_plan): whole head tiles (<= 64 strata) or head tiles in a
 # few chunks, the last tiles in 8x finer chunks.  rt_multi_render reproduces
 # the plan per shard, so the frame stays bit-identical; the plan only changes
-# the fp64 summation grouping against the uniform split (RTX_TAIL_TILES=0).
+# the fp64 summation grouping against the uniform split (rt_tuning.tail_tiles < 0).
 PLAN_CASES = [("three_spheres.json", 4), ("bouncing_seed42.json", 100)]
 
 
@@ -122,11 +122,8 @@ def test_multi_render_head_tail_plan_bit_identical(scene, spp):
     f = camera_frame(S.camera_desc(image_width=1920, samples_per_pixel=spp, max_depth=6))
     with Renderer(S, device=0) as R:
         one = R.render(f, seed=4)
-        os.environ["RTX_TAIL_TILES"] = "0"
-        try:
-            uniform = R.render(f, seed=4)
-        finally:
-            del os.environ["RTX_TAIL_TILES"]
+    with Renderer(S, device=0, tuning={"tail_tiles": -1.0}) as R:
+        uniform = R.render(f, seed=4)
     np.testing.assert_allclose(one, uniform, rtol=1e-12, atol=1e-14)
     for shards in (2, 3):
         with MultiRenderer(S, devices=(0,), shards=shards) as M:
