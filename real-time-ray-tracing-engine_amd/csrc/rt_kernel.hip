@@ -382,7 +382,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
           ps.sample = s_first + (item >> 6);
           key.pixel = (uint32_t)(j * Cr.W + i);
           key.sample = (uint32_t)ps.sample;
-          ps.ray = camera_ray<F == F_FLAT, RT_KCONST_MODE(F)>(Cr, key, i, j, ps.sample);
+          ps.ray = camera_ray<RT_KB_F(F), RT_KCONST_MODE(F)>(Cr, key, i, j, ps.sample);
           ps.T = v3(1.0, 1.0, 1.0);
           ps.bounce = 0;
           ps.active = Cr.max_depth > 0;

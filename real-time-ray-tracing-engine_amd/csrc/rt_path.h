@@ -165,6 +165,9 @@ RT_HD RT_FI uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return a ^ b ^ c;
 #endif
 }
+// the key barrier per instance: the plain flat one only (every instance with
+// it: C4 -8.6 %, C3 -0.5 %, C2 +-0.5 %, profiles/r05e_kb_ab.log)
+#define RT_KB_F(F) ((F) == F_FLAT)
 template <bool KB = false>
 RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                          uint32_t k0, uint32_t k1, uint32_t out[4]) {
@@ -928,6 +931,7 @@ RT_HD RT_FI int box_span(const DScene &S, const DMedium &M, const Ray &mr, doubl
 // the winning medium once, after every medium has been tested.
 // (box_path, STATS: 1 box_span decided, 0 box_span deferred to boundary_span,
 // -1 not a box)
+template <bool KB = false>
 RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin,
                     double tmax, const Key &key, uint32_t bounce, double &hit_t,
                     int &box_path) {
@@ -945,7 +949,7 @@ RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin
   double rl = sqrt(len2(r.d));
   double inside = (t2 - t1) * rl;
   double uu[4];
-  u01x4(key, bounce, kSlotMediumBase + (uint32_t)M.id, uu);
+  u01x4<KB>(key, bounce, kSlotMediumBase + (uint32_t)M.id, uu);
   double hd = M.neg_inv_density * log(uu[0]);
   if (hd > inside) return false;
   hit_t = t1 + hd / rl;
@@ -1420,7 +1424,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
       if (STATS) cnt.other++;
       double tm_hit;
       int box_path;
-      const bool mh = medium_t(S, S.mitems[m], r, tmin, closest, key, bounce, tm_hit, box_path);
+      const bool mh = medium_t<RT_KB_F(F)>(S, S.mitems[m], r, tmin, closest, key, bounce, tm_hit, box_path);
       if (STATS) {
         cnt.mbox += box_path >= 0;
         cnt.mbox_fb += box_path == 0;
@@ -1487,6 +1491,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
     q = ray_f32<kFma>(r);
     tmin32 = f32_dn(tmin);
   }
+
   // hit test of world item ii against ray rr (|d|^2 = ra, its reciprocal ry)
   // in (tmin, tmax): the root in t
   // (uniform: UTag<true> where ii is the same in every lane -- the flat walk)
@@ -1996,7 +2001,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
     return false;
   }
   double rn[4]; // one block per shading event: (e0, e1, d0, d1)
-  u01x4<F == F_FLAT>(key, b, kSlotShade, rn);
+  u01x4<RT_KB_F(F)>(key, b, kSlotShade, rn);
   const double e0 = rn[0], e1 = rn[1], d0 = rn[2], d1 = rn[3];
   const Ray &r = ps.ray;
   constexpr bool kMerge = RT_SHADE_MERGE_F(F);
