@@ -7,8 +7,15 @@ sharding, each the best of `reps` launches, and adds the library kernels the
 N>1 timed region runs besides the render: each rank's chunk sum
 (rt_tiles_sum_device) and, on rank 0, the tile -> frame reorder
 (rt_tiles_to_frame_device).  Prints the slowest rank's time, the compute-only
-speedup t(1) / max(rank) and the gather payload per rank.  The RCCL gather
-itself (1/N of the frame per rank over xGMI) is not included.
+speedup t(1) / max(rank) and the gather payload per rank, and prices the RCCL
+gather: 1/N of the frame per rank, every rank on its own xGMI link into rank 0
+at --link-gbs (default 64 GB/s one way, a conservative share of a link's ~76
+GB/s per direction): `gather_ms`.  bench.py double-buffers, so the gather of
+frame k overlaps frame k+1's render; what a K-step timed region cannot hide
+is the last frame's gather, `speedup_k` = t(1) / (max(rank) + gather / K) for
+K = 20 (the driver's step count).  Rank 0's path-trip lane use (STATS: the
+share of lane slots of the path loop with a live path; a unit's end drains
+it) is reported per N.
 
     python tools/shard_sim.py [--config C2] [--reps 3] [--n 1 2 4 8] [--units U ...]
 (--units: work-unit targets of the chunk choice, rtx.dist.auto_chunks; one
@@ -49,6 +56,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--n", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--units", type=int, nargs="+", default=[None])
+    ap.add_argument("--link-gbs", type=float, default=64.0)
+    ap.add_argument("--k", type=int, default=20)
     a = ap.parse_args()
     name, width, spp, depth = CONFIGS[a.config]
     S = load_scene(os.path.join(SCENES, name + ".json"))
@@ -78,13 +87,18 @@ def main():
                 b, e = r * strata // N, (r + 1) * strata // N
                 st.append(timed(lambda: R.render_device(f, frame.data_ptr(), 0, samples=(b, e - b),
                                                         output=abi.RT_OUT_SUM, accumulate=0), a.reps))
+            gbytes = t_r * 64 * 3 * 8
+            gather = 0.0 if N == 1 else gbytes / (a.link_gbs * 1e9) * 1e3
+            st0 = R.stats(f, seed=0, tiles=(0, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
             print(json.dumps({
                 "config": a.config, "N": N, "t1_ms": round(t1, 3), "units_target": U, "tiles_chunks": ch,
                 "tiles_rank_ms": [round(x, 3) for x in per_rank],
                 "tiles_chunk_sum_ms": None if ch == 1 else "included per rank",
                 "tiles_reorder_ms_rank0": round(t_frame, 3),
                 "tiles_ms": round(tiles_max, 3), "tiles_speedup": round(t1 / tiles_max, 2),
-                "gather_bytes_per_rank": t_r * 64 * 3 * 8,
+                "gather_bytes_per_rank": gbytes, "gather_ms": round(gather, 3),
+                "speedup_k": round(t1 / (tiles_max + gather / a.k), 2),
+                "rank0_path_trip_lane_use": round(st0["segments"] / max(1, 64 * st0["wave_trips"]), 4),
                 "strata_rank_ms": [round(x, 3) for x in st], "strata_ms": round(max(st), 3),
                 "strata_speedup": round(t1 / max(st), 2)}), flush=True)
 
