@@ -179,7 +179,7 @@ def test_ctypes_mirror_matches_header_compiled_layout(tmp_path):
              (abi.ObjectDesc, "rt_object_desc"), (abi.SceneDesc, "rt_scene_desc"),
              (abi.CameraDesc, "rt_camera_desc"), (abi.Frame, "rt_frame"),
              (abi.RenderParams, "rt_render_params"), (abi.PathStats, "rt_path_stats"),
-             (abi.SceneInfo, "rt_scene_info")]
+             (abi.SceneInfo, "rt_scene_info"), (abi.Tuning, "rt_tuning")]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt_api.h"', "int main(void) {"]
     want = []
     for py, cn in pairs:
@@ -197,3 +197,13 @@ def test_ctypes_mirror_matches_header_compiled_layout(tmp_path):
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
                                           text=True).stdout.split()]
     assert got == want
+
+
+def test_tuning_from_a_dict_and_unknown_fields():
+    """rt_tuning through the Python binding: a dict of field names (zero =
+    the default plan), an unknown field refused rather than ignored."""
+    t = abi.tuning({"chunk_target": -1, "tail_tiles": 0.25, "no_lds_perlin": 1})
+    assert t.chunk_target == -1 and t.tail_tiles == 0.25 and t.no_lds_perlin == 1
+    assert t.grid_cap == 0 and abi.tuning(None) is None and abi.tuning(t) is t
+    with pytest.raises(KeyError):
+        abi.tuning({"chunk_targt": 1})
