@@ -1911,8 +1911,11 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
   return sum;
 }
 
-template <int KC = 0>
-RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double r2) {
+// SC: sincos(2 pi r1) arrives precomputed in (sp1, cp1) -- the caller's one
+// sincos shared with the other shading branches (shade, RT_SHADE_SINCOS)
+template <int KC = 0, bool SC = false>
+RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double r2,
+                       double sp1 = 0.0, double cp1 = 0.0) {
   int k = S.n_lights - 1;
   for (int i = 0; i < S.n_lights; ++i)
     if (upick < S.lights[i].cum) {
@@ -1932,8 +1935,8 @@ RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double 
     V3 vv = unitv(cross(w, a));
     V3 uu = cross(w, vv);
     double z = 1 + r2 * (sqrt(1 - s.rr / d2) - 1);
-    double sphi, cphi;
-    sincos_2pi<KC>(r1, sphi, cphi);
+    double sphi = sp1, cphi = cp1;
+    if constexpr (!SC) sincos_2pi<KC>(r1, sphi, cphi);
     double x = cphi * sqrt(1 - z * z);
     double y = sphi * sqrt(1 - z * z);
     d = ((x * uu) + (y * vv)) + (z * w);
@@ -1985,6 +1988,9 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 // pure overhead) -2 %, C4 -1 % (more spills): merged in the plain BVH instances only.
 #ifndef RT_SHADE_MERGE_F
 #define RT_SHADE_MERGE_F(F) (RT_SHADE_MERGE != 0 && ((F) & ~F_BVH4) == 0)
+#endif
+#ifndef RT_SHADE_SINCOS
+#define RT_SHADE_SINCOS 1
 #endif
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
@@ -2117,16 +2123,38 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   if constexpr ((F & F_LIGHTS) != 0) have_lights = S.n_lights > 0;
   V3 gd;
   bool from_light = false;
+  // one sincos(2 pi a) for whichever of the light sample (a sphere light's
+  // azimuth, a = d0), the cosine direction (a = d0) and the isotropic
+  // direction (a = d1) a lane takes: the wave runs it once instead of once
+  // per branch that any lane takes -- the same operation on the same operand
+  // for every lane (RT_SHADE_SINCOS; the merged-shading instances have theirs).
+  // C4 +2.4 %, frames bit-identical (profiles/r05h_*).
+  constexpr bool kSc = RT_SHADE_SINCOS && !kMerge && (F & F_LIGHTS) != 0;
+  [[maybe_unused]] double sps = 0.0, cps = 0.0;
+  if constexpr (kSc) {
+    const bool to_light = e0 < 0.5 && have_lights;
+    sincos_2pi<RT_KCONST_MODE(F)>((to_light || lamb) ? d0 : d1, sps, cps);
+  }
   if constexpr ((F & F_LIGHTS) != 0) {
     if (e0 < 0.5 && have_lights) {
       const uint64_t t0 = STATS ? clk() : 0;
-      gd = lights_random<RT_KCONST_MODE(F)>(S, h.p, e1, d0, d1);
+      gd = lights_random<RT_KCONST_MODE(F), kSc>(S, h.p, e1, d0, d1, sps, cps);
       from_light = true;
       if (STATS && wave_once()) cnt.clights += clk() - t0;
     }
   }
   if (!from_light) {
-    if (kMerge) { // the shared sincos and first root (above)
+    if (kSc) {
+      if (lamb) { // random_cosine_direction, Vec3Utility.hpp:94-103
+        double sr = sqrt_n(d1);
+        V3 lc = v3(cps * sr, sps * sr, sqrt_n(1 - d1));
+        gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
+      } else {
+        double z = 1.0 - 2.0 * d0;
+        double rr = sqrt_n(fmax(0.0, 1.0 - z * z));
+        gd = v3(rr * cps, rr * sps, z);
+      }
+    } else if (kMerge) { // the shared sincos and first root (above)
       if (lamb) {
         V3 lc = v3(cp1 * s1, sp1 * s1, sqrt_n(1 - d1));
         gd = ((lc.x * ou) + (lc.y * ov)) + (lc.z * w);
