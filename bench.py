@@ -402,7 +402,8 @@ def other_configs(args, torch, dev, skip, pmcs):
     it an 8-GPU config; one GPU renders the whole frame here), timed like the
     headline (device-resident frame buffer, single rank, K steps bracketed by
     device syncs, HIP-event kernel time), so the bench line carries every
-    config; C3 also with its own roofline (live PMC passes when available)."""
+    config; C3 and C4 also with their own roofline (live PMC passes when
+    available)."""
     from rtx import abi
     from rtx.render import Renderer, camera_frame
     from rtx.scene import load_scene
@@ -607,10 +608,12 @@ def main():
         if pmc and args.pmc_save:
             with open(args.pmc_save, "w") as fh:
                 json.dump(dict(pmc, config=args.config), fh, indent=1)
-        if full_line and args.config != "C3":
-            pmc_other["C3"] = pmc_live(args, "C3")
-    if full_line and args.config != "C3":
-        pmc_other["C3"] = load_pmc(args, "C3", pmc_other.get("C3"))
+        for c in ("C3", "C4"):  # the other configs with their own live roofline
+            if full_line and args.config != c:
+                pmc_other[c] = pmc_live(args, c)
+    for c in ("C3", "C4"):
+        if full_line and args.config != c:
+            pmc_other[c] = load_pmc(args, c, pmc_other.get(c))
     import torch
     from rtx import abi
     from rtx.render import Renderer, camera_frame
