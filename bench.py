@@ -731,9 +731,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    host_s = 0.0  # host time spent issuing the steps (the launch side of the pipeline)
     for k in range(args.steps):
+        h0 = time.perf_counter()
         step(k, k)
-        if ws == 1:
+        host_s += time.perf_counter() - h0
+        if not use_pg:
             kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
     drain()
     torch.cuda.synchronize(dev)
@@ -752,7 +755,7 @@ def main():
         check = {"max_abs_diff": err, "ok": bool(err <= 1e-9 * scale)}
 
     diag = None
-    if ws > 1:  # kernel time measured after the timed region (no sync inside it)
+    if use_pg:  # kernel time measured after the timed region (no sync inside it)
         for k in range(min(2, args.steps)):
             launch_work(5000 + k, 0)
             kernel_ms.append(R.last_kernel_ms())
@@ -768,7 +771,7 @@ def main():
                      chunks=shard.chunks)
     else:
         st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
-    px_launch = shard.tiles_per_rank * shard.chunks * 64 if tiles_mode else W * H
+    px_launch = shard.tiles_per_rank * max(1, shard.chunks) * 64 if tiles_mode else W * H
     bytes_launch = algorithmic_bytes(st, info, px_launch)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
@@ -806,6 +809,8 @@ def main():
                     "N>1 lines carry no PMC data (traffic null)"
                     if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")
 
+    units_desc = ("library head/tail units, RT_CHUNKS_AUTO" if tiles_mode and shard.library_units
+                  else "%d stratum chunks" % shard.chunks if tiles_mode else "")
     out = {
         "metric": BASELINE["metric"],
         "value": round(value, 3),
@@ -821,10 +826,10 @@ def main():
         "data": "synthetic: JSON scene %s, seeded Philox sample stream" % name,
         "config": {"workload": "%s %s %dx%d spp%d depth%d" % (args.config, name, W, H, n_strata, depth),
                    "scene": name, "width": W, "height": H, "spp": n_strata, "max_depth": depth,
-                   "parallelism": (("1 GPU, tile work units x%d chunks" % shard.chunks
+                   "parallelism": (("1 GPU, tile work units (%s)" % units_desc
                                     if tiles_mode else "1 GPU") if not use_pg else
-                                   "tile-shard x%d (tile t on rank t %% %d, %d stratum chunks) + %s gather" % (
-                                       ws, ws, shard.chunks,
+                                   "tile-shard x%d (tile t on rank t %% %d, %s) + %s gather" % (
+                                       ws, ws, units_desc,
                                        "RCCL" if args.backend == "nccl" else "gloo")
                                    if tiles_mode else
                                    "stratum-shard x%d + %s reduce(sum)" % (
@@ -835,6 +840,10 @@ def main():
         out["check"] = check
     if diag is not None:
         out["ranks"] = diag
+    # rank 0's host time per step in the timed loop: with N>1 the steps are
+    # issued without a sync, so the host keeps ahead while this stays below
+    # ms_per_step
+    out["host_issue_ms_per_step"] = round(host_s * 1e3 / args.steps, 3)
     if rank == 0 and full_line:
         out["other_configs"] = other_configs(args, torch, dev, args.config, pmc_other)
         if not tiles_mode:

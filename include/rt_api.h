@@ -75,8 +75,11 @@ extern "C" {
       rt_multi exchange runs on the devices.
    4: rt_tuning with rt_scene_create_tuned / rt_multi_create_tuned (the
       library reads no environment variables); rt_path_stats.medium_box_*;
-      rt_scene_info.lds_node_bytes. */
-#define RT_ABI_VERSION 4
+      rt_scene_info.lds_node_bytes.
+   5: strata_chunks = RT_CHUNKS_AUTO (rt_render_device, RT_LAYOUT_TILES): the
+      library's work units for a tile subset, per-tile sums out; rt_tuning
+      sub_* fields (in three of the reserved slots: same size and offsets). */
+#define RT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define RT_OK 0
@@ -261,8 +264,16 @@ typedef struct rt_render_params {
                             many equal consecutive chunks, each traced by its own
                             wavefront (finer work units for small tile subsets);
                             the output becomes [tile k][chunk c][64 px][3], whose
-                            chunk sums are the tile's sums.  0 or 1 = one chunk. */
+                            chunk sums are the tile's sums.  0 or 1 = one chunk.
+                            RT_CHUNKS_AUTO (rt_render_device only, with RT_OUT_SUM
+                            and accumulate 0): the library splits the subset into
+                            work units sized to the device (a head/tail plan: the
+                            last tiles in finer chunks, taken last) and returns
+                            the per-tile sums [tile k][64 px][3], the chunk
+                            partials added on the device in chunk order on the
+                            same stream. */
 } rt_render_params;
+#define RT_CHUNKS_AUTO (-1)
 
 /* Per-launch traversal/shading counters (for algorithmic-bytes accounting). */
 typedef struct rt_path_stats {
@@ -378,7 +389,12 @@ typedef struct rt_tuning {
   int32_t sah_leaf_max, sah_leaf_split; /* host SAH leaf rules; 0: the builder's defaults */
   int32_t sah_trav_x4, sah_bins;        /* host SAH traversal cost x4, bins; 0: 4, 16 */
   int32_t extra_features;   /* RT_FEAT_* bits OR'ed into the kernel instance key (debug) */
-  int32_t reserved[7];
+  /* tile-subset work units (rt_render_device, strata_chunks = RT_CHUNKS_AUTO);
+     subsets of more than 4 tiles per wave slot take the frame plan above */
+  int32_t sub_head_strata;   /* strata per head unit; 0: 16 x sqrt(strata / 64) */
+  int32_t sub_tail_split;    /* tail chunks per head chunk; 0: 2 */
+  int32_t sub_tail_permille; /* tail tiles per 1000 wave slots; 0: 250; < 0: none */
+  int32_t reserved[4];
 } rt_tuning;
 
 int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **scene);

@@ -666,6 +666,59 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   return sp;
 }
 
+// Work units of a tile-subset launch that returns its tiles' sums
+// (strata_chunks = RT_CHUNKS_AUTO: one rank's share of a tile-sharded frame).
+// A share of more than 4 tiles per wave slot takes the frame plan.  A smaller
+// one (an 8-way rank of a 1080p frame: 4,050 tiles on 4,096 slots) cannot
+// hand whole tiles to the waves -- the slowest tile would be the launch -- so
+// every tile is split into head units of `sub_head_strata` strata, and the
+// last sub_tail_permille / 1000 x slots tiles into `sub_tail_split` times
+// finer chunks, which the waves take last (dispatch / counter order) so the
+// launch ends on short units.  Long units drain less often (a unit ends with
+// its last paths finishing while lanes idle), short ones balance the end.
+// Defaults from 8-way sweeps on one GPU (profiles/r05n_*, r05o_*): head units
+// of 16 x sqrt(strata / 64) strata (C2 16, C3 32, C4 64), a tail of a quarter
+// of the slots' tiles in halves of those: against every tile in the rank's
+// uniform chunks, C2's share -3 to -8 %, C3's -1.5 %, C4's -0.8 %.
+constexpr int kSubTailSplit = 2, kSubTailPermille = 250;
+static SplitPlan subset_plan(const rt_scene *s, const DLaunch &L) {
+  SplitPlan sp{L.n_local_tiles, 1, 1};
+  if (L.sample_count < 2 || L.n_local_tiles < 1 || s->wave_slots <= 0) return sp;
+  const rt_tuning &tu = s->tune;
+  const int64_t tiles = (int64_t)L.n_local_tiles,
+                slots = s->pc_grid > 0 && s->ds.pc_waves > 0 ? (int64_t)s->pc_grid * s->ds.pc_waves : s->wave_slots;
+  if (tiles > 4 * slots) {
+    DLaunch F = L;
+    F.compact = 0;
+    F.tile_first = 0;
+    F.tile_stride = 1;
+    return frame_plan(s, F);
+  }
+  auto no_empty = [&](int64_t c) { // chunk count with no empty chunks
+    c = std::max<int64_t>(1, std::min<int64_t>(c, L.sample_count));
+    const int64_t cs = (L.sample_count + c - 1) / c;
+    return (int)((L.sample_count + cs - 1) / cs);
+  };
+  const int head = tu.sub_head_strata > 0
+                       ? tu.sub_head_strata
+                       : std::max(1, (int)std::lround(16.0 * std::sqrt(L.sample_count / 64.0)));
+  const int split = tu.sub_tail_split > 0 ? tu.sub_tail_split : kSubTailSplit;
+  const int permille = tu.sub_tail_permille != 0 ? tu.sub_tail_permille : kSubTailPermille;
+  sp.head_chunks = no_empty((L.sample_count + head - 1) / head);
+  sp.chunks = sp.head_chunks;
+  sp.n_head = (int)tiles;
+  if (permille > 0) {
+    const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, slots * permille / 1000));
+    const int tc = no_empty((int64_t)split * sp.head_chunks);
+    if (tc > sp.head_chunks) {
+      sp.chunks = tc;
+      sp.n_head = (int)(tiles - n_tail);
+    }
+  }
+  if (sp.n_head == 0) sp.head_chunks = 1; // every tile a tail tile
+  return sp;
+}
+
 static int ensure_scratch(rt_scene *s, size_t bytes) {
   if (s->scratch_bytes >= bytes) return RT_OK;
   if (s->scratch) {
@@ -763,32 +816,53 @@ int rt_render(rt_scene *s, const rt_frame *f, const rt_render_params *p, double 
 
 int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, double *dev_rgb,
                      void *hip_stream) {
-  if (!s || !dev_rgb) return set_err(RT_ERR_INVALID, "null argument");
+  if (!s || !dev_rgb || !p) return set_err(RT_ERR_INVALID, "null argument");
   DCamera C;
   DLaunch L;
+  const bool auto_units = p->strata_chunks == RT_CHUNKS_AUTO;
+  if (auto_units && (p->layout != RT_LAYOUT_TILES || p->output != RT_OUT_SUM || p->accumulate))
+    return set_err(RT_ERR_INVALID, "RT_CHUNKS_AUTO returns raw tile sums: RT_LAYOUT_TILES, "
+                                   "RT_OUT_SUM, accumulate 0");
+  rt_render_params q = *p;
+  if (auto_units) q.strata_chunks = 0;
   int rc = to_device_camera(f, C);
   if (rc) return rc;
-  if ((rc = to_launch(f, p, L))) return rc;
+  if ((rc = to_launch(f, &q, L))) return rc;
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)hip_stream; // NULL = the HIP null stream (HIP convention)
-  return launch(s, C, L, dev_rgb, nullptr, st);
+  if (!auto_units) return launch(s, C, L, dev_rgb, nullptr, st);
+  // the subset's own units: whole head tiles straight into dev_rgb, chunk
+  // partials into the scratch, added in chunk order into dev_rgb (the
+  // rt_multi shards' finish), all on `st`
+  const SplitPlan sp = subset_plan(s, L);
+  if ((rc = launch(s, C, L, dev_rgb, nullptr, st, &sp))) return rc;
+  hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
+                                         dev_rgb, st);
+  if (e != hipSuccess) return hip_err(e, "tile chunk sum");
+  return RT_OK;
 }
 
 int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
                     rt_path_stats *stats) {
-  if (!s || !stats) return set_err(RT_ERR_INVALID, "null argument");
+  if (!s || !stats || !p) return set_err(RT_ERR_INVALID, "null argument");
   DCamera C;
   DLaunch L;
+  // RT_CHUNKS_AUTO: the counters of the subset plan's own units
+  const bool auto_units = p->strata_chunks == RT_CHUNKS_AUTO && p->layout == RT_LAYOUT_TILES;
+  rt_render_params q = *p;
+  if (auto_units) q.strata_chunks = 0;
   int rc = to_device_camera(f, C);
   if (rc) return rc;
-  if ((rc = to_launch(f, p, L))) return rc;
+  if ((rc = to_launch(f, &q, L))) return rc;
   DeviceGuard g(s->device);
   L.accumulate = 0;
   size_t n = out_doubles(f, L);
   if ((rc = ensure_out(s, n * sizeof(double)))) return rc;
   hipError_t e = hipMemsetAsync(s->stats, 0, RT_N_STATS * sizeof(unsigned long long), s->stream);
   if (e != hipSuccess) return hip_err(e, "hipMemsetAsync stats");
-  if ((rc = launch(s, C, L, s->out_buf, s->stats, s->stream))) return rc;
+  SplitPlan sp{};
+  if (auto_units) sp = subset_plan(s, L);
+  if ((rc = launch(s, C, L, s->out_buf, s->stats, s->stream, auto_units ? &sp : nullptr))) return rc;
   unsigned long long h[RT_N_STATS];
   e = hipMemcpyAsync(h, s->stats, sizeof h, hipMemcpyDeviceToHost, s->stream);
   if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync stats");

@@ -5,7 +5,7 @@ sizes against the compiled library's own view (rt_abi_sizes) when available.
 """
 import ctypes as C
 
-RT_ABI_VERSION = 4  # include/rt_api.h; rtx/lib.py refuses a library of another version
+RT_ABI_VERSION = 5  # include/rt_api.h; rtx/lib.py refuses a library of another version
 
 RT_OK = 0
 RT_ERR_INVALID = -1
@@ -97,6 +97,7 @@ class RenderParams(C.Structure):
 
 
 RT_LAYOUT_FRAME, RT_LAYOUT_TILES = 0, 1
+RT_CHUNKS_AUTO = -1  # strata_chunks: the library's units for a tile subset, per-tile sums out
 
 
 class PathStats(C.Structure):
@@ -137,7 +138,9 @@ class Tuning(C.Structure):
                 ("sah_stack_budget", C.c_int32), ("lbvh_max_depth", C.c_int32),
                 ("sah_leaf_max", C.c_int32), ("sah_leaf_split", C.c_int32),
                 ("sah_trav_x4", C.c_int32), ("sah_bins", C.c_int32),
-                ("extra_features", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("extra_features", C.c_int32),
+                ("sub_head_strata", C.c_int32), ("sub_tail_split", C.c_int32),
+                ("sub_tail_permille", C.c_int32), ("reserved", C.c_int32 * 4)]
 
 
 def tuning(t=None):

@@ -10,12 +10,15 @@ Two decompositions of one frame over the ranks of the default process group:
   from each rank, over all of rank 0's xGMI links at once) and reorders them
   into the frame on its device (rt_tiles_to_frame_device): the timed region
   runs library kernels and the RCCL gather, no framework ops.
-  Every pixel is computed by exactly one GPU.  Its strata are split into the
-  rank's own chunk count (`auto_chunks`, sized for each rank's wave slots), not
-  the one-GPU frame launch's, so a pixel's chunk partials are added in a
-  different grouping: the frame equals the one-GPU frame up to fp64 summation
-  order (the 2-rank rehearsal measures 2.8e-14).  The C ABI's rt_multi_render
-  (strata_chunks 0) keeps the frame launch's split and is bit-identical.
+  Every pixel is computed by exactly one GPU.  A rank's work units are the
+  library's (strata_chunks = RT_CHUNKS_AUTO: head chunks sized to the strata,
+  the last tiles in finer chunks, the chunk sum inside the call), or every
+  tile in `auto_chunks` chunks when a unit target is given.  Either split
+  groups a pixel's strata differently from the one-GPU frame launch (but for
+  a rank holding more than 4 tiles per wave slot, which takes the frame plan),
+  so the frame equals the one-GPU frame up to fp64 summation order (the 2-rank
+  rehearsal measures ~1e-14).  The C ABI's rt_multi_render (strata_chunks 0)
+  keeps the frame launch's split and is bit-identical.
 * stratum sharding (below): ranks split the strata and reduce(sum) full-frame
   accumulators — the SURVEY §8(e) recommendation; it moves ~2x the frame per
   rank through a ring and changes the fp64 summation order.
@@ -148,13 +151,15 @@ class TileShardedRenderer:
     """Renders one frame per call with tile t on rank t % world.
 
     render_fn(frame, buf, seed, tiles=(first, stride), chunks) must overwrite
-    `buf` ([T_r, chunks, 64, 3] float64) with the raw sums of all strata of
-    those tiles in RT_LAYOUT_TILES order, each tile's strata split into
-    `chunks` (Renderer.render_device with output=RT_OUT_SUM, accumulate=0,
-    layout=RT_LAYOUT_TILES, chunks=chunks).  The chunk sum and the tile ->
-    frame reorder are the library's device kernels (tiles_sum(parts, out),
-    to_frame(gathered, frame, out)); the CPU tests pass torch equivalents for
-    their host tensors."""
+    `buf` with the raw sums of all strata of those tiles in RT_LAYOUT_TILES
+    order (Renderer.render_device with output=RT_OUT_SUM, accumulate=0,
+    layout=RT_LAYOUT_TILES, chunks=chunks): with chunks = RT_CHUNKS_AUTO (the
+    default: no `chunks`, no `target_units`) `buf` is [T_r, 64, 3], the tile
+    sums of the library's own work units; otherwise [T_r, chunks, 64, 3], each
+    tile's strata split into `chunks`, added by tiles_sum(parts, out).  The
+    chunk sum and the tile -> frame reorder are the library's device kernels
+    (tiles_sum, to_frame(gathered, frame, out)); the CPU tests pass torch
+    equivalents for their host tensors."""
 
     def __init__(self, render_fn, frame, rank=0, world=1, chunks=None, tiles_sum=None,
                  to_frame=None, target_units=None):
@@ -162,11 +167,17 @@ class TileShardedRenderer:
         self.frame = frame
         self.rank, self.world = rank, world
         self.n_tiles, self.tiles_per_rank = tile_counts(frame, world)
-        self.chunks = auto_chunks(frame, world, target_units) if chunks is None else max(1, chunks)
+        self.library_units = chunks is None and target_units is None
+        if self.library_units:
+            self.chunks = abi.RT_CHUNKS_AUTO
+        else:
+            self.chunks = auto_chunks(frame, world, target_units) if chunks is None else max(1, chunks)
         self.tiles_sum = tiles_sum or device_tiles_sum
         self.to_frame = to_frame or device_tiles_to_frame
 
     def buffer(self, device=None):
+        if self.library_units:  # the tile sums themselves
+            return self.sum_buffer(device)
         return torch.zeros((self.tiles_per_rank, self.chunks, 64, 3), dtype=torch.float64,
                            device=device)
 
@@ -185,6 +196,8 @@ class TileShardedRenderer:
         """Render this rank's tiles; returns the per-tile sums [T_r, 64, 3] (the
         chunk sum, in fixed chunk order) in `out` (a sum_buffer)."""
         self.render_fn(self.frame, buf, seed, (self.rank, self.world), self.chunks)
+        if self.library_units:
+            return buf
         if self.chunks == 1:
             return buf[:, 0]
         return self.tiles_sum(buf, out if out is not None else self.sum_buffer(buf.device))

@@ -154,6 +154,33 @@ def test_shard_chunks_follow_the_strata():
     assert auto_chunks(f, 8, 4096) == 2  # 4,050 tiles per rank: 2 chunks reach 4096 units
 
 
+def test_tile_shards_default_to_the_library_units():
+    """No chunk count and no unit target: each rank asks the library for its
+    own units (strata_chunks = RT_CHUNKS_AUTO) and gets the tile sums back, so
+    the buffer is the sum buffer and no chunk sum follows."""
+    from rtx.render import camera_frame
+    S = load_scene(SCENE)
+    f = camera_frame(S.camera_desc(image_width=27, samples_per_pixel=4, max_depth=6))
+    seen = []
+
+    def render_fn(fr, buf, seed, tiles, chunks):
+        seen.append((tuple(buf.shape), tiles, chunks))
+        buf.fill_(float(tiles[0] + 1))
+
+    def no_sum(parts, out):
+        raise AssertionError("library units need no chunk sum")
+
+    tr = TileShardedRenderer(render_fn, f, 1, 3, tiles_sum=no_sum)
+    assert tr.library_units and tr.chunks == abi.RT_CHUNKS_AUTO
+    buf = tr.buffer()
+    got = tr.render(buf, seed=2)
+    assert got is buf and seen == [((tr.tiles_per_rank, 64, 3), (1, 3), abi.RT_CHUNKS_AUTO)]
+    assert torch.equal(got, torch.full((tr.tiles_per_rank, 64, 3), 2.0, dtype=torch.float64))
+    # a unit target (bench.py --shard-units) keeps the uniform chunks + chunk sum
+    tr2 = TileShardedRenderer(render_fn, f, 1, 3, target_units=64)
+    assert not tr2.library_units and tr2.buffer().shape[1] == tr2.chunks >= 1
+
+
 def _tile_worker(rank, world, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

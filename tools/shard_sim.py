@@ -58,49 +58,87 @@ def main():
     ap.add_argument("--units", type=int, nargs="+", default=[None])
     ap.add_argument("--link-gbs", type=float, default=64.0)
     ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--rank-order", default="fwd", choices=["fwd", "rev"],
+                    help="order the ranks' shares are timed in (rev: a check that the "
+                         "per-rank spread is content, not the GPU's clock history)")
+    ap.add_argument("--rank-work", action="store_true",
+                    help="also report each rank's path segments and wave trips (STATS)")
+    ap.add_argument("--plan", default="chunks", choices=["chunks", "auto"],
+                    help="chunks: every tile in rtx.dist.auto_chunks chunks + the chunk sum "
+                         "(--units); auto: strata_chunks = RT_CHUNKS_AUTO, the library's "
+                         "head/tail units for the subset, tile sums out")
+    ap.add_argument("--tuning", nargs="+", default=[None],
+                    help="rt_tuning dicts as JSON (one scene per entry), e.g. "
+                         "'{\"sub_head_strata\": 32}'")
+    ap.add_argument("--strata-sharding", action="store_true",
+                    help="also time the stratum-sharded split")
     a = ap.parse_args()
     name, width, spp, depth = CONFIGS[a.config]
     S = load_scene(os.path.join(SCENES, name + ".json"))
     f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=depth))
     strata = f.sqrt_spp ** 2
     frame = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda")
-    with Renderer(S) as R:
-        t1 = timed(lambda: R.render_device(f, frame.data_ptr(), 0, output=abi.RT_OUT_SUM,
-                                           accumulate=0), a.reps)
-        for N, U in [(N, U) for N in a.n for U in a.units]:
-            n, t_r = tile_counts(f, N)
-            ch = auto_chunks(f, N, U)
-            buf = torch.empty((t_r, ch, 64, 3), dtype=torch.float64, device="cuda")
-            sums = torch.empty((t_r, 64, 3), dtype=torch.float64, device="cuda")
-            gath = torch.zeros((N, t_r, 64, 3), dtype=torch.float64, device="cuda")
-            per_rank = []
-            for r in range(N):
-                tr = timed(lambda: R.render_device(f, buf.data_ptr(), 0, output=abi.RT_OUT_SUM,
-                                                   accumulate=0, tiles=(r, N),
-                                                   layout=abi.RT_LAYOUT_TILES, chunks=ch), a.reps)
-                ts = timed(lambda: device_tiles_sum(buf, sums), a.reps) if ch > 1 else 0.0
-                per_rank.append(tr + ts)
-            t_frame = timed(lambda: device_tiles_to_frame(gath, f, frame), a.reps)
-            tiles_max = max(per_rank[0] + t_frame, max(per_rank))
-            st = []
-            for r in range(N):
-                b, e = r * strata // N, (r + 1) * strata // N
-                st.append(timed(lambda: R.render_device(f, frame.data_ptr(), 0, samples=(b, e - b),
-                                                        output=abi.RT_OUT_SUM, accumulate=0), a.reps))
-            gbytes = t_r * 64 * 3 * 8
-            gather = 0.0 if N == 1 else gbytes / (a.link_gbs * 1e9) * 1e3
-            st0 = R.stats(f, seed=0, tiles=(0, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
-            print(json.dumps({
-                "config": a.config, "N": N, "t1_ms": round(t1, 3), "units_target": U, "tiles_chunks": ch,
-                "tiles_rank_ms": [round(x, 3) for x in per_rank],
-                "tiles_chunk_sum_ms": None if ch == 1 else "included per rank",
-                "tiles_reorder_ms_rank0": round(t_frame, 3),
-                "tiles_ms": round(tiles_max, 3), "tiles_speedup": round(t1 / tiles_max, 2),
-                "gather_bytes_per_rank": gbytes, "gather_ms": round(gather, 3),
-                "speedup_k": round(t1 / (tiles_max + gather / a.k), 2),
-                "rank0_path_trip_lane_use": round(st0["segments"] / max(1, 64 * st0["wave_trips"]), 4),
-                "strata_rank_ms": [round(x, 3) for x in st], "strata_ms": round(max(st), 3),
-                "strata_speedup": round(t1 / max(st), 2)}), flush=True)
+    for tj in a.tuning:
+        tune = json.loads(tj) if tj else None
+        with Renderer(S, tuning=tune) as R:
+            t1 = timed(lambda: R.render_device(f, frame.data_ptr(), 0, output=abi.RT_OUT_SUM,
+                                               accumulate=0), a.reps)
+            units = a.units if a.plan == "chunks" else [None]
+            for N, U in [(N, U) for N in a.n for U in units]:
+                print(json.dumps(dict(case(a, R, f, frame, strata, t1, N, U), tuning=tune)), flush=True)
+
+
+def case(a, R, f, frame, strata, t1, N, U):
+    n, t_r = tile_counts(f, N)
+    auto = a.plan == "auto"
+    ch = abi.RT_CHUNKS_AUTO if auto else auto_chunks(f, N, U)
+    sums = torch.empty((t_r, 64, 3), dtype=torch.float64, device="cuda")
+    buf = sums if auto else torch.empty((t_r, ch, 64, 3), dtype=torch.float64, device="cuda")
+    gath = torch.zeros((N, t_r, 64, 3), dtype=torch.float64, device="cuda")
+
+    def share(r):
+        R.render_device(f, buf.data_ptr(), 0, output=abi.RT_OUT_SUM, accumulate=0,
+                        tiles=(r, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
+        if not auto and ch > 1:
+            device_tiles_sum(buf, sums)
+
+    per_rank = [0.0] * N
+    for r in range(N):  # one untimed pass over every share first: the first
+        # share timed after a change of launch shape otherwise reads slow
+        # (r05m: the same rank fast in reverse order)
+        share(r)
+    for r in (range(N) if a.rank_order == "fwd" else range(N - 1, -1, -1)):
+        per_rank[r] = timed(lambda: share(r), a.reps)  # render + chunk sum
+    t_frame = timed(lambda: device_tiles_to_frame(gath, f, frame), a.reps)
+    tiles_max = max(per_rank[0] + t_frame, max(per_rank))
+    gbytes = t_r * 64 * 3 * 8
+    gather = 0.0 if N == 1 else gbytes / (a.link_gbs * 1e9) * 1e3
+    st0 = R.stats(f, seed=0, tiles=(0, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
+    out = {
+        "config": a.config, "N": N, "t1_ms": round(t1, 3), "plan": a.plan,
+        "units_target": U, "tiles_chunks": "library" if auto else ch,
+        "tiles_rank_ms": [round(x, 3) for x in per_rank],
+        "tiles_chunk_sum_ms": "included per rank",
+        "tiles_reorder_ms_rank0": round(t_frame, 3),
+        "tiles_ms": round(tiles_max, 3), "tiles_speedup": round(t1 / tiles_max, 2),
+        "gather_bytes_per_rank": gbytes, "gather_ms": round(gather, 3),
+        "speedup_k": round(t1 / (tiles_max + gather / a.k), 2),
+        "rank0_path_trip_lane_use": round(st0["segments"] / max(1, 64 * st0["wave_trips"]), 4),
+        "rank_order": a.rank_order}
+    if a.rank_work:
+        sts = [st0] + [R.stats(f, seed=0, tiles=(r, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
+                       for r in range(1, N)]
+        out.update(rank_segments=[x["segments"] for x in sts],
+                   rank_wave_trips=[x["wave_trips"] for x in sts])
+    if a.strata_sharding:
+        st = []
+        for r in range(N):
+            b, e = r * strata // N, (r + 1) * strata // N
+            st.append(timed(lambda: R.render_device(f, frame.data_ptr(), 0, samples=(b, e - b),
+                                                    output=abi.RT_OUT_SUM, accumulate=0), a.reps))
+        out.update(strata_rank_ms=[round(x, 3) for x in st], strata_ms=round(max(st), 3),
+                   strata_speedup=round(t1 / max(st), 2))
+    return out
 
 
 if __name__ == "__main__":
