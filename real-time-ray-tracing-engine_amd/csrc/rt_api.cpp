@@ -401,17 +401,7 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
   d.root_is_leaf = H.root_is_leaf;
   d.n_root_items = H.n_root_items;
   d.static_spheres = rtx::all_spheres_static(H);
-  d.features = 0;
-  if (!H.mitems.empty()) d.features |= RT_FEAT_MEDIA;
-  for (const DItem &it : H.items)
-    if (it.xf_count) d.features |= RT_FEAT_XFORM;
-  for (const DItem &it : H.mitems)
-    if (it.xf_count) d.features |= RT_FEAT_XFORM;
-  for (const DLight &L : H.lights)
-    if (L.xf_count) d.features |= RT_FEAT_XFORM;
-  if (!H.lights.empty()) d.features |= RT_FEAT_LIGHTS;
-  for (const DTex &t : H.texs)
-    if (t.kind == RT_TEX_NOISE) d.features |= RT_FEAT_NOISE;
+  d.features = rtx::scene_features(H);
   d.features |= tune.extra_features & 15; // debug: widen the instance
   // device-built world BVH (rt_bvh_build.hip), host SAH fallback if the linear
   // tree is deeper than the traversal stack

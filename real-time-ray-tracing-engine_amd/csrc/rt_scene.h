@@ -49,6 +49,25 @@ inline int32_t all_spheres_static(const HostScene &H) {
   return 1;
 }
 
+// The feature bits of the path-tracer instance a compiled scene needs
+// (RT_FEAT_MEDIA / XFORM / LIGHTS / NOISE; RT_FEAT_FLAT and RT_FEAT_BVH4 follow
+// from the world tree once it is built): the GPU library's choice and the CPU
+// backend's (host/rtx_cpu.cpp) alike.
+inline int32_t scene_features(const HostScene &H) {
+  int32_t f = 0;
+  if (!H.mitems.empty()) f |= RT_FEAT_MEDIA;
+  for (const DItem &it : H.items)
+    if (it.xf_count) f |= RT_FEAT_XFORM;
+  for (const DItem &it : H.mitems)
+    if (it.xf_count) f |= RT_FEAT_XFORM;
+  for (const DLight &L : H.lights)
+    if (L.xf_count) f |= RT_FEAT_XFORM;
+  if (!H.lights.empty()) f |= RT_FEAT_LIGHTS;
+  for (const DTex &t : H.texs)
+    if (t.kind == RT_TEX_NOISE) f |= RT_FEAT_NOISE;
+  return f;
+}
+
 // Scenes with at least this many world primitives build their BVH on the
 // device when rt_scene_desc.bvh_builder is RT_BVH_AUTO.
 constexpr int kDeviceBuildMin = 65536;

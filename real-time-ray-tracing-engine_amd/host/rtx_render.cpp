@@ -8,12 +8,20 @@
 //   rtx_render [--camera static] [--output image.ppm] [-p] [-b] [-g] [-d]
 //              [--width N] [--samples N] [--depth N]
 //              [--scene file.json] [--seed S] [--device D] [--gpus N] [--shards K]
-//              [--dump-desc]
+//              [--backend hip|cpu] [--threads N] [--dump-desc]
 //
 // Mapping of the reference flags onto this library:
 //   --camera static   the only mode; "dynamic" is the SDL window (out of scope,
 //                     DESIGN.md) and is rejected with a message.
-//   -p / -g           accepted; rendering is always the parallel GPU path.
+//   -p / -g           accepted; the backend is --backend's (default hip: the GPU
+//                     library).  The reference's -p without -g selects its CPU
+//                     path; here that is --backend cpu.
+//   --backend cpu     the CPU backend (librtx_cpu.so, include/rt_cpu.h): the
+//                     kernel's per-path source compiled for the host, image rows
+//                     on --threads N host threads (default: one per hardware
+//                     thread; StaticCamera::render_cpu's ThreadPool role,
+//                     StaticCamera.cpp:32-134).  Chosen, never a fallback: the
+//                     default backend fails if the GPU library cannot render.
 //   -b                scene use_bvh (the reference's light-list BVH split); the
 //                     world BVH is always built on the device.
 //   -d                writes the flattened scene description to logs/scene_desc.json
@@ -35,6 +43,7 @@
 // the frame into K tile shards, K > N putting several shards on one device.
 // The sharded frame is bit-identical to the one-device frame (rt_api.h).
 #include "rt_api.h"
+#include "rt_cpu.h"
 #include "scene_json.hpp"
 
 #include <chrono>
@@ -58,6 +67,8 @@ struct Options {
   unsigned long long seed = 0;
   int device = 0;
   int gpus = 1, shards = 0;
+  bool cpu = false; // --backend cpu
+  int threads = 0;  // --threads (CPU backend); 0: one per hardware thread
 };
 
 bool parse_int(const char *s, int &out) {
@@ -105,8 +116,18 @@ Options parse(int argc, char **argv) {
       o.gpu = true;
     } else if (a == "-d" || a == "--debug") {
       o.debug = true;
+    } else if (a == "--backend") {
+      if (const char *b = need("an argument: hip or cpu")) {
+        std::string be = b;
+        if (be == "hip" || be == "gpu") o.cpu = false;
+        else if (be == "cpu") o.cpu = true;
+        else {
+          o.any_errors = true;
+          std::cerr << "Unknown backend: " << be << " (hip or cpu)\n";
+        }
+      }
     } else if (a == "--width" || a == "--samples" || a == "--depth" || a == "--device" ||
-               a == "--gpus" || a == "--shards") {
+               a == "--gpus" || a == "--shards" || a == "--threads") {
       if (const char *v = need("a number")) {
         int x;
         if (!parse_int(v, x)) {
@@ -125,6 +146,8 @@ Options parse(int argc, char **argv) {
           o.gpus = x;
         } else if (a == "--shards") {
           o.shards = x;
+        } else if (a == "--threads") {
+          o.threads = x;
         } else {
           o.device = x;
         }
@@ -144,6 +167,14 @@ Options parse(int argc, char **argv) {
     o.any_errors = true;
     std::cerr << "--gpus must be >= 1 and --shards >= --gpus\n";
   }
+  if (o.threads < 0) {
+    o.any_errors = true;
+    std::cerr << "--threads must be >= 0\n";
+  }
+  if (o.cpu && (o.gpus > 1 || o.shards > 1)) {
+    o.any_errors = true;
+    std::cerr << "--gpus / --shards are GPU options; --backend cpu uses --threads\n";
+  }
   if (!o.use_static && output_selected)
     std::cerr << "You can only set an output file if the static camera is selected, ignoring...\n";
   return o;
@@ -157,9 +188,9 @@ void print_help() {
          "  -h, --help                 Show this help message\n"
          "  --camera [static|dynamic]  Camera type (default: static; dynamic is not provided)\n"
          "  --output <file>            Output file under output/ (default: image.ppm)\n"
-         "  -p, --parallel             Accepted (rendering is always parallel on the GPU)\n"
+         "  -p, --parallel             Accepted (both backends are parallel)\n"
          "  -b, --bvh                  Use the reference's BVH light-list split (use_bvh)\n"
-         "  -g, --gpu                  Accepted (rendering is always on the GPU)\n"
+         "  -g, --gpu                  Accepted (the default backend is the GPU)\n"
          "  -d, --debug                Write the scene description to logs/scene_desc.json\n"
          "  --width <int>              Image width (default: 600)\n"
          "  --samples <int>            Samples per pixel (default: 100)\n"
@@ -169,6 +200,8 @@ void print_help() {
          "  --device <int>             HIP device ordinal (default: 0)\n"
          "  --gpus <int>               Devices to render on, from --device (default: 1)\n"
          "  --shards <int>             Tile shards over those devices (default: --gpus)\n"
+         "  --backend <hip|cpu>        GPU library (default) or the CPU backend\n"
+         "  --threads <int>            CPU backend threads (default: one per hardware thread)\n"
          "  --dump-desc                Print the flattened scene description and exit\n";
 }
 
@@ -348,7 +381,13 @@ int main(int argc, char **argv) {
   rt_scene *scene = nullptr;
   rt_multi *multi = nullptr;
   const int shards = opt.shards ? opt.shards : opt.gpus;
-  if (shards > 1) {
+  if (opt.cpu) {
+    if (rt_cpu_abi_version() != RT_CPU_ABI_VERSION) {
+      std::cerr << "[ERROR] librtx_cpu ABI version " << rt_cpu_abi_version() << ", this host was built for "
+                << RT_CPU_ABI_VERSION << "\n";
+      return 1;
+    }
+  } else if (shards > 1) {
     int32_t ndev = 0;
     if (rt_device_count(&ndev) != RT_OK) return fail_rt("device count");
     if (opt.device < 0 || opt.device + opt.gpus > ndev) {
@@ -384,8 +423,13 @@ int main(int argc, char **argv) {
     p.sample_count = cnt;
     p.seed = opt.seed;
     p.output = RT_OUT_SUM;
-    if ((multi ? rt_multi_render(multi, &frame, &p, part.data())
-               : rt_render(scene, &frame, &p, part.data())) != RT_OK) {
+    if (opt.cpu) {
+      if (rt_cpu_render(&desc, &frame, &p, opt.threads, part.data()) != RT_OK) {
+        std::cerr << "[ERROR] render: " << rt_cpu_last_error() << "\n";
+        return 1;
+      }
+    } else if ((multi ? rt_multi_render(multi, &frame, &p, part.data())
+                      : rt_render(scene, &frame, &p, part.data())) != RT_OK) {
       int rc = fail_rt("render");
       release();
       return rc;
@@ -397,7 +441,8 @@ int main(int argc, char **argv) {
   release();
   std::clog << "\rDone. " << W << "x" << H << " @ " << n_strata << " spp, "
             << (double)W * H * n_strata / secs / 1e6 << " Msamples/s";
-  if (shards > 1) std::clog << " (" << shards << " tile shards on " << opt.gpus << " device(s))";
+  if (opt.cpu) std::clog << " (CPU backend)";
+  else if (shards > 1) std::clog << " (" << shards << " tile shards on " << opt.gpus << " device(s))";
   std::clog << "\n";
 
   mkdir("output", 0755);

@@ -17,9 +17,22 @@ HEADER = os.path.join(O.ROOT, "include", "rt_api.h")
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def header_functions():
-    txt = open(HEADER).read()
+def header_functions(header=HEADER):
+    txt = open(header).read()
     return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(rt_\w+)\s*\(", txt, re.M)))
+
+
+def test_cpu_backend_header_symbols_are_exported():
+    """include/rt_cpu.h (the CLI's --backend cpu) is served by librtx_cpu.so,
+    not by the GPU library."""
+    cpu_h = os.path.join(O.ROOT, "include", "rt_cpu.h")
+    lib = os.path.join(os.path.dirname(LIB_PATH), "librtx_cpu.so")
+    declared = header_functions(cpu_h)
+    assert declared == ["rt_cpu_abi_version", "rt_cpu_last_error", "rt_cpu_render"]
+    L = C.CDLL(lib)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert not any(hasattr(C.CDLL(LIB_PATH), n) for n in declared)
 
 
 def test_library_built_and_loads():
