@@ -50,8 +50,12 @@ extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double s
                                           uint8_t *bytes, hipStream_t stream);
 extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
                                            hipStream_t stream);
+extern "C" int rtk_tile_order_f(int features);
+extern "C" hipError_t rtk_launch_tile_order(const uint32_t *cost, int n, int n_head, int32_t *order,
+                                            hipStream_t stream);
 extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
-                                              int n_chunks, double *out, hipStream_t stream);
+                                              int n_chunks, const int32_t *order, double *out,
+                                              hipStream_t stream);
 extern "C" hipError_t rtk_launch_tiles_to_frame(const double *tiles, int n_shards, int64_t shard_stride,
                                                 int W, int row_begin, int row_end, double scale, int scaled,
                                                 int accumulate, double *out, hipStream_t stream);
@@ -75,6 +79,14 @@ struct rt_scene {
   int pc_grid = 0;           // resident blocks of the persistent instance on this device
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
   rt_tuning tune{};          // explicit tuning (rt_scene_create_tuned; zero: the default plan)
+  // cost-ordered dispatch ("tile order", launch()): per-tile unit costs of the
+  // last launch and the two order buffers (the one a launch reads, the one the
+  // sort after it writes for the next launch of the same shape)
+  uint32_t *tile_cost = nullptr;
+  int32_t *tile_order[2] = {nullptr, nullptr};
+  int order_cap = 0, order_cur = 0;
+  bool order_ready = false;
+  int32_t order_sig[10] = {};
 };
 
 namespace {
@@ -177,6 +189,8 @@ int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
   L.chunk_strata = (L.sample_count + chunks - 1) / chunks;
   L.unit_ctr = nullptr;
   L.grid_cap = 0;
+  L.tile_order = nullptr;
+  L.tile_cost = nullptr;
   // one chunk: every tile is a whole unit; strata_chunks > 1 (tile layout):
   // every tile split, its chunk partials are the caller's output (the launcher
   // points parts at the output buffer)
@@ -572,6 +586,9 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->out_buf) (void)hipFree(s->out_buf);
   if (s->scratch) (void)hipFree(s->scratch);
+  if (s->tile_cost) (void)hipFree(s->tile_cost);
+  if (s->tile_order[0]) (void)hipFree(s->tile_order[0]);
+  if (s->tile_order[1]) (void)hipFree(s->tile_order[1]);
   if (s->block) (void)hipFree(s->block);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -723,11 +740,52 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
   return RT_OK;
 }
 
+// Cost-ordered dispatch ("tile order"): a launch's work units are taken in
+// plan order (head units, then the finer tail chunks -- unit index order is
+// the dispatcher's and the persistent counter's order), so the launch ends on
+// whatever tiles come last.  Tiles differ several-fold in cost (sky vs glass,
+// r05t: C2's units 0.2-2.5 ms at one device), and a costly tile met last
+// keeps its wave slot busy while the others idle: the one-device C2 frame
+// spent 7.7 % of its slot-time idle, an 8-way rank's share 14.5 %.  So each
+// launch measures its tiles' costs (units add their durations per tile) and a
+// one-block sort after it orders the tiles most expensive first for the next
+// launch of the same shape (longest processing time first): the plan's k-th
+// tile is then tile_order[k].  The head tiles are ordered among themselves and
+// the tail tiles among themselves (the tail still last), so every tile keeps
+// its own split into units -- whole, head chunks or tail chunks -- and so its
+// summation grouping: only the schedule moves, and the frames are
+// bit-identical with and without it (rt_tuning.no_tile_order,
+// tests/test_tile_order.py).  (Ordering across the split, so the cheapest
+// tiles became the tail, regrouped those tiles' sums: not bit-identical.)
+static int ensure_order(rt_scene *s, int n) {
+  if (s->order_cap >= n) return RT_OK;
+  if (s->tile_cost) {
+    (void)hipDeviceSynchronize(); // a launch on any stream may still use them
+    (void)hipFree(s->tile_cost);
+    (void)hipFree(s->tile_order[0]);
+    (void)hipFree(s->tile_order[1]);
+  }
+  s->tile_cost = nullptr;
+  s->tile_order[0] = s->tile_order[1] = nullptr;
+  s->order_cap = 0;
+  s->order_ready = false;
+  hipError_t e = hipMalloc((void **)&s->tile_cost, (size_t)n * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc((void **)&s->tile_order[0], (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc((void **)&s->tile_order[1], (size_t)n * sizeof(int32_t));
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc tile order: ") + hipGetErrorString(e));
+  s->order_cap = n;
+  return RT_OK;
+}
+
 // forced: the split plan of a tile-layout launch whose whole tiles go to
 // dev_out (compact) and split tiles' raw partials to the scene's scratch
-// (rt_multi_render's shards, reproducing the one-device frame's units)
+// (rt_multi_render's shards, reproducing the one-device frame's units).
+// *order_used: the dispatch order the launch used (null: plan order) -- what a
+// finish kernel run after it must map the plan's tiles with.
 static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_out,
-                  unsigned long long *stats, hipStream_t st, const SplitPlan *forced = nullptr) {
+                  unsigned long long *stats, hipStream_t st, const SplitPlan *forced = nullptr,
+                  const int32_t **order_used = nullptr) {
+  if (order_used) *order_used = nullptr;
   const SplitPlan sp = forced ? *forced : stats ? SplitPlan{L.n_local_tiles, 1, 1} : frame_plan(s, L);
   const size_t n_parts = plan_parts(sp, L.n_local_tiles);
   const bool split = !L.compact && n_parts > 0;
@@ -745,6 +803,26 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
                                  : std::max(1, s->wave_slots / std::max(1, s->ds.pc_waves));
     // rt_tuning.grid_cap: fewer resident blocks (tests: many units per wave)
     if (s->tune.grid_cap > 0) Lp.grid_cap = s->tune.grid_cap;
+  }
+  // cost-ordered dispatch: frame launches and forced / library plans, not the
+  // STATS instance nor a caller's explicit chunk layout (its partials are the
+  // output, by plan tile)
+  const bool ordered = !s->tune.no_tile_order && stats == nullptr && (forced || !L.parts_final) &&
+                       L.n_local_tiles > 1 && rtk_tile_order_f(s->ds.features);
+  const int32_t sig[10] = {L.n_local_tiles, L.tile_first, L.tile_stride, L.tiles_x, L.row_begin,
+                           L.row_end,       L.sample_count, sp.n_head,   sp.head_chunks, sp.chunks};
+  bool use_order = false;
+  if (ordered) {
+    int rc = ensure_order(s, L.n_local_tiles);
+    if (rc) return rc;
+    use_order = s->order_ready && std::equal(sig, sig + 10, s->order_sig);
+    Lp.tile_order = use_order ? s->tile_order[s->order_cur] : nullptr;
+    Lp.tile_cost = s->tile_cost;
+    hipError_t me = hipMemsetAsync(s->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
+    if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
+  } else {
+    Lp.tile_order = nullptr;
+    Lp.tile_cost = nullptr;
   }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
@@ -765,6 +843,16 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   e = hipEventRecord(s->ev1, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   s->timed = true;
+  if (ordered) { // the next launch's order, into the buffer this one did not read
+    const int next = s->order_cur ^ 1;
+    e = rtk_launch_tile_order(s->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
+                              s->tile_order[next], st);
+    if (e != hipSuccess) return hip_err(e, "tile order");
+    if (order_used) *order_used = Lp.tile_order;
+    s->order_cur = next;
+    s->order_ready = true;
+    std::copy(sig, sig + 10, s->order_sig);
+  }
   return RT_OK;
 }
 
@@ -825,9 +913,10 @@ int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, 
   // partials into the scratch, added in chunk order into dev_rgb (the
   // rt_multi shards' finish), all on `st`
   const SplitPlan sp = subset_plan(s, L);
-  if ((rc = launch(s, C, L, dev_rgb, nullptr, st, &sp))) return rc;
+  const int32_t *order = nullptr;
+  if ((rc = launch(s, C, L, dev_rgb, nullptr, st, &sp, &order))) return rc;
   hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
-                                         dev_rgb, st);
+                                         order, dev_rgb, st);
   if (e != hipSuccess) return hip_err(e, "tile chunk sum");
   return RT_OK;
 }
@@ -1084,9 +1173,10 @@ static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *
   DeviceGuard g(s->device);
   const size_t nt = (size_t)L.n_local_tiles * 64 * 3;
   if ((rc = ensure_out(s, std::max<size_t>(nt, 1) * sizeof(double)))) return rc;
-  if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream, &sp))) return rc;
+  const int32_t *order = nullptr;
+  if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream, &sp, &order))) return rc;
   hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
-                                         s->out_buf, s->stream);
+                                         order, s->out_buf, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return hip_err(e, "shard render");
   *t_done = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();

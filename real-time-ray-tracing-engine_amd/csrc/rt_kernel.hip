@@ -130,15 +130,16 @@ struct KArgs {
 // on the GPU: tests/test_persistent.py, and through every BASELINE band).
 static_assert(sizeof(DScene) == 160 && alignof(DScene) == 8, "DScene kernarg layout");
 static_assert(sizeof(DCamera) == 208 && alignof(DCamera) == 8, "DCamera kernarg layout");
-static_assert(sizeof(DLaunch) == 96 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
+static_assert(sizeof(DLaunch) == 112 && alignof(DLaunch) == 8, "DLaunch kernarg layout");
 static_assert(offsetof(KArgs, S) == 0 && offsetof(KArgs, C) == 160 && offsetof(KArgs, P) == 368 &&
-                  offsetof(KArgs, out) == 464 && offsetof(KArgs, stats) == 472 &&
-                  sizeof(KArgs) == 480,
+                  offsetof(KArgs, out) == 480 && offsetof(KArgs, stats) == 488 &&
+                  sizeof(KArgs) == 496,
               "KArgs must mirror render_tiles' kernarg layout");
 static_assert(offsetof(DLaunch, n_chunks) == 56 && offsetof(DLaunch, unit_ctr) == 64 &&
                   offsetof(DLaunch, grid_cap) == 72 && offsetof(DLaunch, n_head) == 76 &&
                   offsetof(DLaunch, parts) == 80 && offsetof(DLaunch, parts_final) == 88 &&
-                  offsetof(DLaunch, head_chunks) == 92,
+                  offsetof(DLaunch, head_chunks) == 92 && offsetof(DLaunch, tile_order) == 96 &&
+                  offsetof(DLaunch, tile_cost) == 104,
               "DLaunch field offsets read from the kernarg segment");
 template <bool FRESH>
 __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
@@ -169,6 +170,8 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
     L.parts = K.parts;
     L.parts_final = K.parts_final;
     L.head_chunks = K.head_chunks;
+    L.tile_order = K.tile_order;
+    L.tile_cost = K.tile_cost;
     return L;
   } else {
     return P;
@@ -213,6 +216,24 @@ __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
     return C;
   }
 }
+// the launch's tile-cost pointer, read at the unit's end from the kernarg
+// segment (not held across the path loop)
+__device__ __forceinline__ uint32_t *tile_cost_arg(const DLaunch &) {
+  auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ka));
+  return ka->P.tile_cost;
+}
+struct UnitRec {
+  unsigned long long t0;
+  int32_t tile, pad;
+};
+// the instances with cost-ordered dispatch (rt_api.cpp "tile order"): the
+// plain flat one (C2) and the plain BVH ones (C3, C5); in the rich instances
+// (C4) its bookkeeping costs registers the path loop needs (C4 -12.5 % for a
+// +1.4 % schedule gain, profiles/r05u_ab.log).  rtk_tile_order_f mirrors it
+// for the host.
+#define RT_ORDER_F(F) ((F) == F_FLAT || ((F) & ~F_BVH4) == 0)
+extern "C" int rtk_tile_order_f(int features) { return RT_ORDER_F((unsigned)features) ? 1 : 0; }
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -223,6 +244,30 @@ __device__ __forceinline__ double *out_arg(double *out) {
     return out;
   }
 }
+
+#ifndef RT_UNIT_TIMES
+#define RT_UNIT_TIMES 0
+#endif
+#if RT_UNIT_TIMES
+// Measurement-only build (make EXTRA=-DRT_UNIT_TIMES=1; tools/unit_timeline.py):
+// every work unit's start and end on the device's constant 100 MHz clock
+// (s_memrealtime), by unit index, for the launch timeline (how long the
+// waves' last units keep the launch open).
+constexpr int kUnitTimesMax = 1 << 21;
+__device__ unsigned long long g_unit_times[2 * kUnitTimesMax];
+extern "C" hipError_t rtk_unit_times(unsigned long long *host, int n_units) {
+  const size_t n = 2 * (size_t)(n_units < kUnitTimesMax ? n_units : kUnitTimesMax);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_unit_times), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost);
+}
+extern "C" hipError_t rtk_unit_times_clear(void) {
+  void *p = nullptr;
+  hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_unit_times));
+  if (e != hipSuccess) return e;
+  e = hipMemset(p, 0, sizeof(g_unit_times));
+  return e != hipSuccess ? e : hipDeviceSynchronize();
+}
+#endif
 
 // PC (persistent): the instance for launches of more units than the grid's
 // resident waves -- frame launches (head units, then the tail chunks) and
@@ -244,6 +289,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
   extern __shared__ int4 dyn_lds[];
   __shared__ double acc_lds[BW][64][3];
+  // the unit's launch tile and start time (tile order / cost, rt_api.cpp):
+  // parked in LDS across the path loop instead of SGPRs
+  __shared__ UnitRec unit_rec[RT_ORDER_F(F) ? BW : 1];
   // compacted leaf tests (BVH instances only; 1 KB per wave)
   __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? BW : 1];
 
@@ -333,6 +381,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     return x;
   };
   while (unit < n_units) { // wave-uniform
+#if RT_UNIT_TIMES
+  const unsigned long long t_unit0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
   // (wave-uniform) head unit: tile unit / head_chunks; tail unit: a chunk of
   // the tail tile n_head + (unit - head units) / n_chunks
@@ -347,6 +398,15 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     local_tile = head ? q : PU.n_head + q;
     s_first = PU.sample_begin + chunk * cs;
     s_count = min(cs, PU.sample_count - chunk * cs);
+  }
+  // the plan's k-th tile -> the launch's local tile (cost-ordered dispatch,
+  // the instances that take it: RT_ORDER_F)
+  if constexpr (RT_ORDER_F(F)) {
+    if (PU.tile_order != nullptr) local_tile = __builtin_amdgcn_readfirstlane(PU.tile_order[local_tile]);
+    if (lane == 0) {
+      unit_rec[wv].tile = local_tile;
+      unit_rec[wv].t0 = PU.tile_cost != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    }
   }
   const int tile = PU.tile_first + local_tile * PU.tile_stride;
   const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
@@ -449,7 +509,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       double *const ob = out_arg<(PC && RT_KARG_FRESH) || kEpiFresh>(out);
       const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
       double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
-                  : PE.compact ? ob + 3 * ((size_t)unit * 64 + lane)
+                  : PE.compact ? ob + 3 * ((size_t)(RT_ORDER_F(F) ? unit_rec[wv].tile : unit) * 64 + lane)
                                : ob + 3 * ((size_t)(j - PE.row_begin) * Ce.W + i);
       if (final_out && PE.accumulate) {
         o[0] += sx;
@@ -463,6 +523,20 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
   }
   __builtin_amdgcn_wave_barrier();
+  // the unit's duration into its tile's cost (the next launch's dispatch order)
+  if constexpr (RT_ORDER_F(F)) {
+    if (lane == 0) {
+      uint32_t *const cost = tile_cost_arg(P);
+      if (cost != nullptr)
+        atomicAdd(&cost[unit_rec[wv].tile], (unsigned)(__builtin_amdgcn_s_memrealtime() - unit_rec[wv].t0));
+    }
+  }
+#if RT_UNIT_TIMES
+  if (lane == 0 && !STATS && unit < kUnitTimesMax) {
+    g_unit_times[2 * unit] = t_unit0;
+    g_unit_times[2 * unit + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if constexpr (!PC) break;
   int next = n_units;
   if (P.unit_ctr != nullptr && lane == 0)
@@ -499,7 +573,8 @@ __global__ void split_sum_kernel(const double *parts, DCamera C, DLaunch P, doub
   const int ch = (int)(idx % 3);
   const int slot = (int)((idx / 3) & 63);
   const int tile = first + (int)(idx / (64 * 3)); // frame launches: tile_first 0, tile_stride 1
-  const int i = (tile % P.tiles_x) * 8 + (slot & 7), j = P.row_begin + (tile / P.tiles_x) * 8 + (slot >> 3);
+  const int pt = P.tile_order != nullptr ? P.tile_order[tile] : tile; // the plan's tile -> the frame's
+  const int i = (pt % P.tiles_x) * 8 + (slot & 7), j = P.row_begin + (pt / P.tiles_x) * 8 + (slot >> 3);
   if (i >= C.W || j >= P.row_end) return;
   const bool head = tile < P.n_head;
   const int nc = head ? P.head_chunks : P.n_chunks;
@@ -536,7 +611,7 @@ __global__ void tiles_sum_kernel(const double *parts, int64_t n_tiles, int chunk
 // are already in out[lt]; each chunked tile's partials (the launch's parts
 // layout, DLaunch) are summed in chunk order into out[lt].
 __global__ void shard_finish_kernel(const double *parts, int n_local, int n_head, int head_chunks,
-                                    int n_chunks, double *out) {
+                                    int n_chunks, const int32_t *order, double *out) {
   const int first = head_chunks > 1 ? 0 : n_head; // first chunked local tile
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)(n_local - first) * kTileD) return;
@@ -549,7 +624,52 @@ __global__ void shard_finish_kernel(const double *parts, int n_local, int n_head
   const double *p = parts + part0 * kTileD + r;
   double sum = p[0];
   for (int c = 1; c < nc; ++c) sum += p[(int64_t)c * kTileD];
-  out[(int64_t)lt * kTileD + r] = sum;
+  out[(int64_t)(order != nullptr ? order[lt] : lt) * kTileD + r] = sum; // the plan's tile -> the launch's
+}
+
+// Cost-ordered dispatch (rt_api.cpp "tile order"): the local tiles sorted by
+// the cost the previous launch of the same shape measured (tile_cost, 100 MHz
+// ticks summed over a tile's units), most expensive first -- the next launch
+// dispatches them in that order (longest processing time first), so its last
+// units are short ones.  Two segments, one block each: the plan's head tiles
+// [0, n_head) among themselves and its tail tiles [n_head, n) among
+// themselves, so every tile keeps its own unit split (whole / head chunks /
+// tail chunks) and so its sums, bit for bit.  Per block: a histogram of 256
+// log-spaced buckets (8 per octave), a descending scan, a scatter; ties land in
+// any order (scheduling only).
+__global__ void tile_order_kernel(const uint32_t *cost, int n, int n_head, int32_t *order) {
+  const int lo = blockIdx.x == 0 ? 0 : n_head, hi = blockIdx.x == 0 ? n_head : n;
+  if (lo >= hi) return;
+  cost += lo;
+  order += lo;
+  n = hi - lo;
+  __shared__ uint32_t hist[256];
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  auto bucket = [](uint32_t c) -> int {
+    if (c == 0) return 0;
+    const int lz = __clz(c);
+    return (31 - lz) * 8 + (int)(((c << lz) >> 28) & 7u);
+  };
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) { // exclusive scan from the top bucket down
+    uint32_t run = 0;
+    for (int k = 255; k >= 0; --k) {
+      const uint32_t c = hist[k];
+      hist[k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[bucket(cost[i])], 1u)] = lo + i;
+}
+
+extern "C" hipError_t rtk_launch_tile_order(const uint32_t *cost, int n, int n_head, int32_t *order,
+                                            hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_order_kernel, dim3(2), dim3(1024), 0, stream, cost, n, n_head, order);
+  return hipGetLastError();
 }
 
 // Compact tiles of n_shards shards -> frame rows [row_begin, row_end): tile t
@@ -781,12 +901,13 @@ extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles,
 }
 
 extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
-                                              int n_chunks, double *out, hipStream_t stream) {
+                                              int n_chunks, const int32_t *order, double *out,
+                                              hipStream_t stream) {
   const int first = head_chunks > 1 ? 0 : n_head;
   const int64_t total = (int64_t)(n_local - first) * kTileD;
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(shard_finish_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, parts, n_local,
-                     n_head, head_chunks, n_chunks, out);
+                     n_head, head_chunks, n_chunks, order, out);
   return hipGetLastError();
 }
 

@@ -272,6 +272,13 @@ struct DLaunch {
   double *parts;
   int32_t parts_final;
   int32_t head_chunks;
+  // Dispatch order (rt_api.cpp "tile order"): the k-th local tile of the plan
+  // above is local tile tile_order[k] of the launch (null: k itself); units,
+  // chunk partials and the head / tail split follow k, every pixel write goes
+  // to the mapped tile.  tile_cost (null: not measured): each unit adds its
+  // duration (100 MHz clock ticks) to its mapped tile's counter.
+  const int32_t *tile_order;
+  uint32_t *tile_cost;
 };
 
 #endif

@@ -140,7 +140,8 @@ class Tuning(C.Structure):
                 ("sah_trav_x4", C.c_int32), ("sah_bins", C.c_int32),
                 ("extra_features", C.c_int32),
                 ("sub_head_strata", C.c_int32), ("sub_tail_split", C.c_int32),
-                ("sub_tail_permille", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("sub_tail_permille", C.c_int32), ("no_tile_order", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 def tuning(t=None):
