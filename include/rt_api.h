@@ -376,7 +376,8 @@ typedef struct rt_tuning {
   int32_t no_uniform_tail; /* 1: no finer last chunks in the uniform split */
   int32_t no_persistent;  /* 1: one work unit per wavefront (no persistent unit loop) */
   int32_t grid_cap;       /* persistent launches: at most this many blocks; 0: every resident one */
-  double tail_tiles;      /* tail tiles per wave slot; 0: 0.5; < 0: no tail plan */
+  double tail_tiles;      /* tail tiles per wave slot; 0: 0.25 (head/tail plan), 0.5 (after the
+                             uniform split); < 0: no tail plan */
   /* LDS staging (rt_scene_create) */
   int32_t lds_nodes;      /* one-unit instances: at most this many BVH nodes; 0: the plan; < 0: none */
   int32_t lds_nodes_pc;   /* the persistent instance's node prefix, the same rule */
@@ -394,7 +395,7 @@ typedef struct rt_tuning {
      subsets of more than 4 tiles per wave slot take the frame plan above */
   int32_t sub_head_strata;   /* strata per head unit; 0: 16 x sqrt(strata / 64) */
   int32_t sub_tail_split;    /* tail chunks per head chunk; 0: 2 */
-  int32_t sub_tail_permille; /* tail tiles per 1000 wave slots; 0: 250; < 0: none */
+  int32_t sub_tail_permille; /* tail tiles per 1000 wave slots; 0: 125; < 0: none */
   int32_t no_tile_order;     /* 1: launches take their tiles in plan order (default: the previous
                                 launch's measured tile costs order them, most expensive first;
                                 the frames are the same bit for bit) */

@@ -605,7 +605,7 @@ int rt_scene_destroy(rt_scene *s) {
 //    slots) whose head plan keeps the partials within 4 frames: head tiles
 //    whole (up to 64 strata: written straight into the frame, C2) or in
 //    chunks of 128 strata (C3: 2 per tile), and the last `slots` x
-//    RTX_TAIL_TILES (default 0.5) tiles in 8x finer chunks, the units the
+//    rt_tuning.tail_tiles (default 0.25) tiles in 8x finer chunks, the units the
 //    waves take last (dispatch / counter order), so the launch ends on a
 //    short unit (C2 +3.9 %, C3 +1.2 % over the uniform split;
 //    profiles/r03f_ab.log).  Whole 256-strata tiles as C3's head: -9 %
@@ -636,6 +636,11 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
     const int64_t cs = (L.sample_count + c - 1) / c;
     return (int)((L.sample_count + cs - 1) / cs);
   };
+  // tail tiles per wave slot: a quarter for the head/tail plan since the head
+  // tiles are taken most expensive first (tile order; C2 +0.9 %, C3 +0.2 %,
+  // profiles/r05x_ab.log), a half after the uniform split (C4 -1.6 % at a
+  // quarter)
+  const double tail_ht = tu.tail_tiles == 0.0 ? 0.25 : std::max(0.0, tu.tail_tiles);
   const double tail = tu.tail_tiles == 0.0 ? 0.5 : std::max(0.0, tu.tail_tiles);
   // head units: whole tiles up to 64 strata (C2); beyond, chunks of 128
   // strata (C3: 2 per tile -- as fast as 4 chunks of 64, half the partial
@@ -647,7 +652,7 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   // chunked tiles + head chunks); otherwise the uniform split
   const bool bounded = head_chunks == 1 || head_chunks * tiles <= 4 * tiles;
   if (tiles > 4 * slots && tail > 0 && bounded) {
-    const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail * slots)));
+    const int64_t n_tail = std::min<int64_t>(tiles, std::max<int64_t>(1, (int64_t)(tail_ht * slots)));
     sp.head_chunks = no_empty((L.sample_count + head_max - 1) / head_max);
     sp.chunks = no_empty(split * (int64_t)sp.head_chunks);
     sp.n_head = (int)(tiles - n_tail);
@@ -657,7 +662,7 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
   const int64_t c = ((int64_t)target * slots + tiles - 1) / std::max<int64_t>(1, tiles);
   sp.chunks = no_empty(c);
   if (sp.chunks > 1) sp.n_head = 0;
-  // ... with the last `slots` x RTX_TAIL_TILES tiles in `split` times finer
+  // ... with the last `slots` x rt_tuning.tail_tiles (default 0.5 here) tiles in `split` times finer
   // chunks when the frame has a tile per wave slot (C4, C5: the uniform
   // units last 15 / 84 ms: C4 +1.7 %, C5 +0.9 %, profiles/r03ae_ab.log;
   // rt_tuning.no_uniform_tail: off, A/B runs)
@@ -684,10 +689,11 @@ static SplitPlan frame_plan(const rt_scene *s, const DLaunch &L) {
 // launch ends on short units.  Long units drain less often (a unit ends with
 // its last paths finishing while lanes idle), short ones balance the end.
 // Defaults from 8-way sweeps on one GPU (profiles/r05n_*, r05o_*): head units
-// of 16 x sqrt(strata / 64) strata (C2 16, C3 32, C4 64), a tail of a quarter
+// of 16 x sqrt(strata / 64) strata (C2 16, C3 32, C4 64), a tail of an eighth
 // of the slots' tiles in halves of those: against every tile in the rank's
-// uniform chunks, C2's share -3 to -8 %, C3's -1.5 %, C4's -0.8 %.
-constexpr int kSubTailSplit = 2, kSubTailPermille = 250;
+// uniform chunks, C2's share -3 to -8 %, C3's -1.5 %, C4's -0.8 % (a quarter
+// then; an eighth since tile order, C2 -3.4 %: profiles/r05x_sim_C2.log).
+constexpr int kSubTailSplit = 2, kSubTailPermille = 125;
 static SplitPlan subset_plan(const rt_scene *s, const DLaunch &L) {
   SplitPlan sp{L.n_local_tiles, 1, 1};
   if (L.sample_count < 2 || L.n_local_tiles < 1 || s->wave_slots <= 0) return sp;
