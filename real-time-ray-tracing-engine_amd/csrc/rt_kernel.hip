@@ -216,17 +216,16 @@ __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
     return C;
   }
 }
-// the launch's tile-cost pointer, read at the unit's end from the kernarg
-// segment (not held across the path loop)
-__device__ __forceinline__ uint32_t *tile_cost_arg(const DLaunch &) {
-  auto ka = (const __attribute__((address_space(4))) KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(ka));
-  return ka->P.tile_cost;
+// The plan's local tile of work unit `unit` (head units: unit / head_chunks;
+// tail units: n_head + (unit - head units) / n_chunks), and the launch's
+// local tile it maps to (cost-ordered dispatch: tile_order; null: itself).
+__device__ __forceinline__ int plan_tile(const DLaunch &L, int unit) {
+  const int head_units = L.n_head * L.head_chunks;
+  return unit < head_units ? unit / L.head_chunks : L.n_head + (unit - head_units) / L.n_chunks;
 }
-struct UnitRec {
-  unsigned long long t0;
-  int32_t tile, pad;
-};
+__device__ __forceinline__ int order_tile(const DLaunch &L, int k) {
+  return L.tile_order != nullptr ? __builtin_amdgcn_readfirstlane(L.tile_order[k]) : k;
+}
 // the instances with cost-ordered dispatch (rt_api.cpp "tile order"): the
 // plain flat one (C2) and the plain BVH ones (C3, C5); in the rich instances
 // (C4) its bookkeeping costs registers the path loop needs (C4 -12.5 % for a
@@ -291,7 +290,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   __shared__ double acc_lds[BW][64][3];
   // the unit's launch tile and start time (tile order / cost, rt_api.cpp):
   // parked in LDS across the path loop instead of SGPRs
-  __shared__ UnitRec unit_rec[RT_ORDER_F(F) ? BW : 1];
   // compacted leaf tests (BVH instances only; 1 KB per wave)
   __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? BW : 1];
 
@@ -400,13 +398,13 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     s_count = min(cs, PU.sample_count - chunk * cs);
   }
   // the plan's k-th tile -> the launch's local tile (cost-ordered dispatch,
-  // the instances that take it: RT_ORDER_F)
+  // the instances that take it: RT_ORDER_F); the unit's cost is its end time
+  // minus its start time, both added to the tile's counter (mod 2^32), so no
+  // start time is held across the path loop
   if constexpr (RT_ORDER_F(F)) {
-    if (PU.tile_order != nullptr) local_tile = __builtin_amdgcn_readfirstlane(PU.tile_order[local_tile]);
-    if (lane == 0) {
-      unit_rec[wv].tile = local_tile;
-      unit_rec[wv].t0 = PU.tile_cost != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    }
+    local_tile = order_tile(PU, local_tile);
+    if (lane == 0 && PU.tile_cost != nullptr)
+      atomicSub(&PU.tile_cost[local_tile], (unsigned)__builtin_amdgcn_s_memrealtime());
   }
   const int tile = PU.tile_first + local_tile * PU.tile_stride;
   const int tx = tile % PU.tiles_x, ty = tile / PU.tiles_x;
@@ -509,7 +507,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       double *const ob = out_arg<(PC && RT_KARG_FRESH) || kEpiFresh>(out);
       const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
       double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
-                  : PE.compact ? ob + 3 * ((size_t)(RT_ORDER_F(F) ? unit_rec[wv].tile : unit) * 64 + lane)
+                  : PE.compact ? ob + 3 * ((size_t)(RT_ORDER_F(F) ? order_tile(PE, unit) : unit) * 64 + lane)
                                : ob + 3 * ((size_t)(j - PE.row_begin) * Ce.W + i);
       if (final_out && PE.accumulate) {
         o[0] += sx;
@@ -526,9 +524,9 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   // the unit's duration into its tile's cost (the next launch's dispatch order)
   if constexpr (RT_ORDER_F(F)) {
     if (lane == 0) {
-      uint32_t *const cost = tile_cost_arg(P);
-      if (cost != nullptr)
-        atomicAdd(&cost[unit_rec[wv].tile], (unsigned)(__builtin_amdgcn_s_memrealtime() - unit_rec[wv].t0));
+      const DLaunch PT = launch_fields<true>(P);
+      if (PT.tile_cost != nullptr)
+        atomicAdd(&PT.tile_cost[order_tile(PT, plan_tile(PT, unit))], (unsigned)__builtin_amdgcn_s_memrealtime());
     }
   }
 #if RT_UNIT_TIMES
