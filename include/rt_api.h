@@ -49,8 +49,10 @@
  * Threading.  Distinct rt_scene objects are independent and may be used from
  * different host threads (and devices) at once.  One rt_scene is used by one
  * host thread at a time: its kernel-timing events, its scratch / staging
- * buffers and its work-unit counter (persistent launches) are per scene.  Asynchronous launches (rt_render_device) on one
- * scene must be ordered by the caller's streams as any device work is.
+ * buffers, its work-unit counter (persistent launches) and its tile-cost /
+ * dispatch-order buffers (rt_tuning.no_tile_order) are per scene.
+ * Asynchronous launches (rt_render_device) on one scene must be ordered by the
+ * caller's streams as any device work is.
  *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
  * random stream is a stateless counter-based Philox4x32-10 keyed by
