@@ -813,8 +813,13 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   // cost-ordered dispatch: frame launches and forced / library plans, not the
   // STATS instance nor a caller's explicit chunk layout (its partials are the
   // output, by plan tile)
+  // ... and launches long enough to pay for the cost memset and the sort: a
+  // progressive frame (one stratum per pixel, ~0.2 ms at 1080p) lost 8-10 %
+  // to them (profiles/r05z_bench_default.json vs r05r's)
+  constexpr int kOrderMinStrata = 16;
   const bool ordered = !s->tune.no_tile_order && stats == nullptr && (forced || !L.parts_final) &&
-                       L.n_local_tiles > 1 && rtk_tile_order_f(s->ds.features);
+                       L.n_local_tiles > 1 && L.sample_count >= kOrderMinStrata &&
+                       rtk_tile_order_f(s->ds.features);
   const int32_t sig[10] = {L.n_local_tiles, L.tile_first, L.tile_stride, L.tiles_x, L.row_begin,
                            L.row_end,       L.sample_count, sp.n_head,   sp.head_chunks, sp.chunks};
   bool use_order = false;

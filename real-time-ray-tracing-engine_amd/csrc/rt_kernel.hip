@@ -229,7 +229,8 @@ __device__ __forceinline__ int order_tile(const DLaunch &L, int k) {
 // the instances with cost-ordered dispatch (rt_api.cpp "tile order"): the
 // plain flat one (C2) and the plain BVH ones (C3, C5); in the rich instances
 // (C4) its bookkeeping costs registers the path loop needs (C4 -12.5 % for a
-// +1.4 % schedule gain, profiles/r05u_ab.log).  rtk_tile_order_f mirrors it
+// +1.4 % schedule gain, profiles/r05u_ab.log; -12.6 % again with the
+// register-free start / end counters, r05z4_c4_order_ab.log).  rtk_tile_order_f mirrors it
 // for the host.
 #define RT_ORDER_F(F) ((F) == F_FLAT || ((F) & ~F_BVH4) == 0)
 extern "C" int rtk_tile_order_f(int features) { return RT_ORDER_F((unsigned)features) ? 1 : 0; }

@@ -28,7 +28,7 @@ def _frames(S, f, tune, seeds, **kw):
 
 
 @pytest.mark.parametrize("name,width,spp,extra", [
-    ("three_spheres", 1920, 4, {}),          # 1080p: whole head tiles + 8x chunked tail
+    ("three_spheres", 1920, 16, {}),         # 1080p: whole head tiles + 8x chunked tail
     ("three_spheres", 200, 16, {}),          # uniform split, every tile chunked
     ("bouncing_seed42", 320, 16, {}),        # persistent instance
     ("bouncing_seed42", 160, 16, {"grid_cap": 3}),
