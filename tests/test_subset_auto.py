@@ -84,3 +84,34 @@ def test_auto_needs_tile_layout_and_raw_sums():
             args.update(kw)
             with pytest.raises(RtError):
                 R.render_device(f, buf.data_ptr(), 0, **args)
+
+
+def test_auto_edge_subsets():
+    """Subsets with no tile at all (a rank past the last tile) and one-stratum
+    launches (whole tiles, no chunk sum) through RT_CHUNKS_AUTO."""
+    S = load_scene(os.path.join(SCENES, "three_spheres.json"))
+    f = camera_frame(S.camera_desc(image_width=16, samples_per_pixel=4, max_depth=4))  # 16x9: 2x2 tiles
+    buf = torch.full((1, 64, 3), 7.0, dtype=torch.float64, device="cuda")
+    with Renderer(S) as R:
+        # tiles (5, 8): tile_first 5 >= the frame's 4 tiles: nothing to render, nothing written
+        R.render_device(f, buf.data_ptr(), 0, seed=1, output=abi.RT_OUT_SUM, accumulate=0,
+                        tiles=(5, 8), layout=abi.RT_LAYOUT_TILES, chunks=abi.RT_CHUNKS_AUTO)
+        torch.cuda.synchronize()
+        assert torch.all(buf == 7.0)
+        # one stratum of every pixel: whole tiles, equal to the frame launch's sums
+        whole = R.render(f, seed=2, output=abi.RT_OUT_SUM, samples=(3, 1))
+        got = _subset_frame_samples(R, f, 2, 2, (3, 1))
+    assert np.array_equal(got, whole)
+
+
+def _subset_frame_samples(R, f, world, seed, samples):
+    _, t_r = tile_counts(f, world)
+    gath = torch.zeros((world, t_r, 64, 3), dtype=torch.float64, device="cuda")
+    for r in range(world):
+        R.render_device(f, gath[r].data_ptr(), 0, seed=seed, samples=samples, output=abi.RT_OUT_SUM,
+                        accumulate=0, tiles=(r, world), layout=abi.RT_LAYOUT_TILES,
+                        chunks=abi.RT_CHUNKS_AUTO)
+    out = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device="cuda")
+    device_tiles_to_frame(gath, f, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
