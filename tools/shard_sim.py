@@ -102,13 +102,17 @@ def case(a, R, f, frame, strata, t1, N, U):
         if not auto and ch > 1:
             device_tiles_sum(buf, sums)
 
-    per_rank = [0.0] * N
-    for r in range(N):  # one untimed pass over every share first: the first
-        # share timed after a change of launch shape otherwise reads slow
-        # (r05m: the same rank fast in reverse order)
-        share(r)
-    for r in (range(N) if a.rank_order == "fwd" else range(N - 1, -1, -1)):
-        per_rank[r] = timed(lambda: share(r), a.reps)  # render + chunk sum
+    # rounds over the ranks, each share launched untimed and then timed: a
+    # rank renders its own share launch after launch, so its timed launch
+    # follows one of the same shape (tile order from that launch's costs);
+    # the best of the rounds per rank (the first share timed after a change
+    # of shape otherwise reads slow -- r05m: the same rank fast in reverse order)
+    per_rank = [None] * N
+    for _ in range(a.reps):
+        for r in (range(N) if a.rank_order == "fwd" else range(N - 1, -1, -1)):
+            share(r)
+            t = timed(lambda: share(r), 1)  # render + chunk sum
+            per_rank[r] = t if per_rank[r] is None else min(per_rank[r], t)
     t_frame = timed(lambda: device_tiles_to_frame(gath, f, frame), a.reps)
     tiles_max = max(per_rank[0] + t_frame, max(per_rank))
     gbytes = t_r * 64 * 3 * 8
