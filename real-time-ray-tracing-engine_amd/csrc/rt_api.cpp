@@ -583,7 +583,9 @@ int rt_scene_info_get(const rt_scene *s, rt_scene_info *info) {
 int rt_scene_destroy(rt_scene *s) {
   if (!s) return RT_OK;
   DeviceGuard g(s->device);
-  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  // launches on caller streams (rt_render_device) may still read the scene's
+  // tables and use its scratch / tile-order buffers: wait for the device
+  (void)hipDeviceSynchronize();
   if (s->out_buf) (void)hipFree(s->out_buf);
   if (s->scratch) (void)hipFree(s->scratch);
   if (s->tile_cost) (void)hipFree(s->tile_cost);
