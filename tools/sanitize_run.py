@@ -15,6 +15,10 @@ sanitizers"; CPU only -- GPU sanitizers are not available on the MI355X pool).
   3. The kernel-source emulator (tests/native/rt_emulate.cpp: rt_path.h and
      rt_scene.cpp built for the host) under ASan/UBSan, driven by
      tests/test_emulator.py with libasan preloaded into the interpreter.
+  4. The CLI's CPU backend (host/rtx_cpu.cpp, round 5) through
+     host/rtx_cpu_check.cpp: its row pool under TSan (8 threads) and its
+     per-path code under ASan/UBSan, every scene rendered twice and the two
+     frames required equal bit for bit.
 
 Writes a log (default profiles/r02_sanitize.log) and exits non-zero on any
 finding.
@@ -129,12 +133,18 @@ def main():
     ap.add_argument("--asan", required=True)
     ap.add_argument("--tsan", required=True)
     ap.add_argument("--emu-asan", default=None)
+    ap.add_argument("--cpu-tsan", default=None)
+    ap.add_argument("--cpu-asan", default=None)
+    ap.add_argument("--only-cpu", action="store_true", help="run step 4 only")
     ap.add_argument("--log", default=os.path.join(ROOT, "profiles", "r02_sanitize.log"))
     ap.add_argument("--per-scene", type=int, default=150)
     a = ap.parse_args()
     log = []
     bad = 0
     scenes = sorted(glob.glob(os.path.join(PKG, "scenes", "*.json")))
+    if a.only_cpu:
+        bad += cpu_backend_steps(a, scenes, log)
+        return finish(a, log, bad)
 
     # 1. valid scenes, ASan/UBSan
     r = run([a.asan] + scenes)
@@ -197,6 +207,25 @@ def main():
         if r.returncode != 0:
             bad += 1
 
+    bad += cpu_backend_steps(a, scenes, log)
+    finish(a, log, bad)
+
+
+def cpu_backend_steps(a, scenes, log):
+    """4. the CPU backend: TSan over its row pool, ASan/UBSan over the path code."""
+    bad = 0
+    for tag, exe, threads in (("tsan", a.cpu_tsan, 8), ("asan", a.cpu_asan, 4)):
+        if not exe:
+            continue
+        r = run([exe, "--threads", str(threads)] + scenes, timeout=1800)
+        log.append("[%s] CPU backend (host/rtx_cpu_check.cpp), %d threads over %d scenes: rc %d\n%s%s" % (
+            tag, threads, len(scenes), r.returncode, r.stdout, r.stderr[-4000:]))
+        if r.returncode != 0 or "Sanitizer" in r.stderr or "runtime error" in r.stderr:
+            bad += 1
+    return bad
+
+
+def finish(a, log, bad):
     log.append("RESULT: %s" % ("clean" if bad == 0 else "%d finding(s)" % bad))
     os.makedirs(os.path.dirname(a.log), exist_ok=True)
     with open(a.log, "w") as f:
