@@ -2,8 +2,10 @@
 """Per-rank device time of an N-way split, measured on ONE GPU (diagnostic).
 
 For N in 1, 2, 4, 8 renders EVERY rank's share under tile sharding (tile t on
-rank t % N, auto stratum chunks -- bench.py's N>1 default) and under stratum
-sharding, each the best of `reps` launches, and adds the library kernels the
+rank t % N; --plan auto, the default: the library's own work units per share,
+RT_CHUNKS_AUTO -- bench.py's N>1 default; --plan chunks: uniform stratum
+chunks per --units target) and optionally under stratum sharding
+(--strata-sharding), each the best of `reps` launches, and adds the library kernels the
 N>1 timed region runs besides the render: each rank's chunk sum
 (rt_tiles_sum_device) and, on rank 0, the tile -> frame reorder
 (rt_tiles_to_frame_device).  Prints the slowest rank's time, the compute-only
@@ -63,7 +65,7 @@ def main():
                          "per-rank spread is content, not the GPU's clock history)")
     ap.add_argument("--rank-work", action="store_true",
                     help="also report each rank's path segments and wave trips (STATS)")
-    ap.add_argument("--plan", default="chunks", choices=["chunks", "auto"],
+    ap.add_argument("--plan", default="auto", choices=["chunks", "auto"],
                     help="chunks: every tile in rtx.dist.auto_chunks chunks + the chunk sum "
                          "(--units); auto: strata_chunks = RT_CHUNKS_AUTO, the library's "
                          "head/tail units for the subset, tile sums out")
