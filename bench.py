@@ -79,6 +79,91 @@ def dist_env():
     return ws, rank, local
 
 
+def visible_devices():
+    """GPUs this process could use, counted without initialising the GPU
+    (torch.cuda.device_count() does not, on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) with no launcher in the environment: this
+    process becomes the launcher.  Before anything touches the GPU it checks
+    that N devices are visible (unless --share-device / --device cpu), then
+    starts N children of this same script with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set (torchrun's
+    variables; one rank per GPU, rank r on cuda:r), relays rank 0's JSON line
+    (rank 0 writes to this process's stdout, every other rank's stdout goes to
+    stderr), and returns non-zero if any rank fails -- the others are then
+    stopped, by their PIDs, rather than left waiting in a collective.  It never
+    re-executes itself.  Returns the exit code."""
+    import signal
+    import socket
+    import subprocess
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if args.device == "cuda" and not args.share_device:
+        n_dev = visible_devices()
+        if n_dev < args.gpus:
+            print("bench: --gpus %d needs %d GPUs, %d visible (one rank per GPU; "
+                  "--share-device puts every rank on cuda:0)" % (args.gpus, args.gpus, n_dev),
+                  file=sys.stderr)
+            return 2
+    port = os.environ.get("MASTER_PORT")
+    if not port:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
+        s.close()
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    stopping = {"sig": None}
+
+    def on_signal(signum, frame):
+        stopping["sig"] = signum
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port, RTX_BENCH_LAUNCHER="bench.py")
+            procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr))
+        print("bench: launched %d ranks (pids %s), MASTER_PORT %s" % (
+            args.gpus, " ".join(str(p.pid) for p in procs), port), file=sys.stderr, flush=True)
+        live = set(range(args.gpus))
+        while live and stopping["sig"] is None:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0:
+                    print("bench: rank %d exited with %d; stopping the other ranks" % (r, code),
+                          file=sys.stderr, flush=True)
+                    rc = code if code > 0 else 128 - code
+                    live.clear()
+                    break
+            time.sleep(0.1)
+        if stopping["sig"] is not None:
+            rc = 128 + stopping["sig"]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
 def algorithmic_bytes(st, info, n_pixels):
     """Bytes the kernel must fetch/store per launch under the device layout
     (SURVEY §8d formula): node fetches x node size + primitive tests x (item +
@@ -593,17 +678,35 @@ def main():
                     help="write the live PMC summary (the pmc_<config>.json format) here")
     ap.add_argument("--shard-units", type=int, default=0,
                     help="N>1 tile shards: work units per rank (0: rtx.dist.shard_units)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: every rank renders with the CPU backend (librtx_cpu.so) and "
+                         "exchanges over gloo -- the launcher / exchange path without a GPU "
+                         "(tests); never the measured line")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: that
+    # rank exits 3 once the process group is up (the launcher must stop the others)
     ap.add_argument("--pmc", default="auto", choices=["auto", "file", "off"],
                     help="N=1 roofline counters: auto = rocprofv3 PMC passes of this build "
                          "run before the timed run (fallback: the committed "
                          "profiles/pmc_<config>.json), file = the committed file only")
     args = ap.parse_args()
+    cpu = args.device == "cpu"
+    if cpu and args.backend != "gloo":
+        print("bench: --device cpu exchanges over gloo (--backend gloo)", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus != 1:
+        # no launcher: start the ranks here (before anything touches the GPU)
+        sys.exit(launch_ranks(args))
 
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        print("bench: --gpus %d but the launcher started WORLD_SIZE %d ranks" % (args.gpus, ws),
+              file=sys.stderr)
+        sys.exit(2)
     pmc = None
-    full_line = ws == 1 and not args.no_other_configs and not args.width and not args.spp
+    full_line = (ws == 1 and not cpu and not args.no_other_configs and not args.width
+                 and not args.spp)
     pmc_other = {}
-    if ws == 1 and args.pmc == "auto":  # before this process initialises the GPU
+    if ws == 1 and args.pmc == "auto" and not cpu:  # before this process initialises the GPU
         pmc = pmc_live(args)
         if pmc and args.pmc_save:
             with open(args.pmc_save, "w") as fh:
@@ -619,19 +722,33 @@ def main():
     from rtx.render import Renderer, camera_frame
     from rtx.scene import load_scene
 
-    if ws != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
     if args.share_device:
         local = 0
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local)
+    if not cpu:
+        torch.cuda.set_device(dev)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize(dev)
     use_pg = ws > 1 or args.pg_rehearsal
+    seen = 1
     if use_pg:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            print("bench: --gpus %d but the process group has %d ranks" % (
+                args.gpus, dist.get_world_size()), file=sys.stderr)
+            sys.exit(2)
+    from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks, ranks_seen
+    if use_pg:  # the ranks the exchange's collective actually reaches (RCCL for nccl)
+        seen = ranks_seen(dev if args.backend == "nccl" else None)
+    if rank == args.fail_rank:
+        print("bench: rank %d failing on request (--fail-rank)" % rank, file=sys.stderr, flush=True)
+        os._exit(3)
 
     name, width, spp, depth = CONFIGS[args.config]
     width = args.width or width
@@ -646,24 +763,31 @@ def main():
     s1 = (rank + 1) * n_strata // ws
     tiles_mode = (use_pg and args.shard == "tiles") or (ws == 1 and args.n1_layout == "tiles")
 
-    from rtx.dist import ShardedRenderer, TileShardedRenderer, max_over_ranks
-    R = Renderer(scene, device=local, tuning=tuning_from_env())
-    info = R.info()
-    stream = torch.cuda.current_stream(dev)  # the null stream: ordered with RCCL's waits
+    if cpu:  # the ranks share this host's CPUs
+        from rtx.cpu import CpuRenderer, default_threads
+        R = CpuRenderer(scene, threads=max(1, default_threads() // ws))
+        info, stream_ptr = None, None
+    else:
+        R = Renderer(scene, device=local, tuning=tuning_from_env())
+        info = R.info()
+        # the null stream: ordered with RCCL's waits
+        stream_ptr = torch.cuda.current_stream(dev).cuda_stream
 
     def render_fn(fr, acc, seed, strata):
         # overwrite the partial sums (no memset, no read-modify-write)
-        R.render_device(fr, acc.data_ptr(), stream.cuda_stream, seed=seed, samples=strata,
+        R.render_device(fr, acc.data_ptr(), stream_ptr, seed=seed, samples=strata,
                         output=abi.RT_OUT_SUM, accumulate=0)
 
     def tile_render_fn(fr, buf, seed, tiles, chunks):
-        R.render_device(fr, buf.data_ptr(), stream.cuda_stream, seed=seed, samples=(0, -1),
+        R.render_device(fr, buf.data_ptr(), stream_ptr, seed=seed, samples=(0, -1),
                         output=abi.RT_OUT_SUM, accumulate=0, tiles=tiles,
                         layout=abi.RT_LAYOUT_TILES, chunks=chunks)
 
     if tiles_mode:
         shard = TileShardedRenderer(tile_render_fn, frame, rank, ws,
                                     target_units=args.shard_units or None)
+        if cpu:
+            shard.on_host()
         bufs = [shard.buffer(dev) for _ in range(2)]
         gath = [shard.gather_buffer(dev) if rank == 0 else None for _ in range(2)]
         sums = [shard.sum_buffer(dev) for _ in range(2)]   # per-tile sums (device chunk sum)
@@ -699,16 +823,16 @@ def main():
         if tiles_mode:
             if args.backend == "nccl":
                 return shard.gather(tsum[b], gath[b], async_op=True)
-            torch.cuda.synchronize(dev)  # gloo: host-staged, no CUDA gather
-            cpu = tsum[b].cpu()
-            parts = [torch.empty_like(cpu) for _ in range(ws)] if rank == 0 else None
-            dist.gather(cpu, gather_list=parts, dst=0)
+            sync()  # gloo: host-staged, no CUDA gather
+            host = tsum[b].cpu()
+            parts = [torch.empty_like(host) for _ in range(ws)] if rank == 0 else None
+            dist.gather(host, gather_list=parts, dst=0)
             if rank == 0:
                 gath[b].copy_(torch.stack(parts))
             return None
         if args.backend == "nccl":
             return dist.reduce(bufs[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
-        torch.cuda.synchronize(dev)  # gloo has no CUDA reduce
+        sync()  # gloo has no CUDA reduce
         return dist.all_reduce(bufs[b], op=dist.ReduceOp.SUM, async_op=True)
 
     def step(k, seed):
@@ -725,11 +849,11 @@ def main():
     for w in range(args.warmup):
         step(w, 1000 + w)
     drain()
-    torch.cuda.synchronize(dev)
+    sync()
 
     if use_pg:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     host_s = 0.0  # host time spent issuing the steps (the launch side of the pipeline)
     for k in range(args.steps):
@@ -739,7 +863,7 @@ def main():
         if not use_pg:
             kernel_ms.append(R.last_kernel_ms())  # HIP events around the kernel, launch stream
     drain()
-    torch.cuda.synchronize(dev)
+    sync()
     if use_pg:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
@@ -749,7 +873,7 @@ def main():
         last = final["frame"].clone()
         ref = torch.empty_like(last)
         render_fn(frame, ref, args.steps - 1, (0, n_strata))
-        torch.cuda.synchronize(dev)
+        sync()
         err = (last - ref).abs().max().item()
         scale = max(1.0, ref.abs().max().item())
         check = {"max_abs_diff": err, "ok": bool(err <= 1e-9 * scale)}
@@ -765,49 +889,58 @@ def main():
     samples_per_step = W * H * n_strata  # whole frame, all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
 
-    # roofline of the dominant (render) kernel on this rank, one launch
-    if tiles_mode:
-        st = R.stats(frame, seed=0, tiles=(rank, ws), layout=abi.RT_LAYOUT_TILES,
-                     chunks=shard.chunks)
+    def gpu_roofline(pmc):
+        # roofline of the dominant (render) kernel on this rank, one launch
+        if tiles_mode:
+            st = R.stats(frame, seed=0, tiles=(rank, ws), layout=abi.RT_LAYOUT_TILES,
+                         chunks=shard.chunks)
+        else:
+            st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
+        px_launch = shard.tiles_per_rank * max(1, shard.chunks) * 64 if tiles_mode else W * H
+        bytes_launch = algorithmic_bytes(st, info, px_launch)
+        avg_ms = sum(kernel_ms) / len(kernel_ms)
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        pmc = load_pmc(args, args.config, pmc) if ws == 1 else None
+        roof = roofline(pmc, avg_ms)
+        roof["cache_served"] = {"bytes_per_launch": int(bytes_launch),
+                                "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
+                                "gbs": round(achieved, 1)}
+        roof["counters"] = st
+        if st.get("cyc_loop"):
+            # STATS instance: shares of a wavefront's loop time per region (s_memtime)
+            roof["phase_share"] = {k[4:]: round(st[k] / st["cyc_loop"], 4) for k in (
+                "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights")}
+        roof["lane_utilisation"] = {
+            "traversal": round(st["node_visits"] / max(1, 64 * st["wave_node_iters"]), 4),
+            "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
+            "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
+            "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
+        if st.get("wave_noise_iters"):
+            roof["lane_utilisation"]["noise_albedo"] = round(
+                st["noise_evals"] / (64 * st["wave_noise_iters"]), 4)
+        if st.get("medium_box_tests"):
+            # box-boundary media: share of their lanes box_span deferred to the
+            # general boundary scan (edge / corner / parallel rays)
+            roof["lane_utilisation"]["medium_box_deferred"] = round(
+                st["medium_box_deferred"] / st["medium_box_tests"], 6)
+        if st.get("model_trace_max"):
+            # the node-loop SIMD model (STATS): one walk per lane per trip vs each
+            # lane's walks of two consecutive trips back to back (two walks per lane)
+            roof["lane_utilisation"]["traversal_model_one_walk"] = round(
+                st["node_visits"] / (64 * st["model_trace_max"]), 4)
+            roof["lane_utilisation"]["traversal_model_two_walks"] = round(
+                st["node_visits"] / (64 * max(1, st["model_trace_pair_max"])), 4)
+        roof["note"] = ("fp64 vector roof (VALU-issue bound, scene LDS/cache resident); "
+                        "N>1 lines carry no PMC data (traffic null)"
+                        if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")
+        return roof
+
+    if cpu:  # the CPU backend's ranks: no kernel, no roof
+        roof = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                "traffic": None, "kernel_ms": round(sum(kernel_ms) / len(kernel_ms), 3),
+                "note": "--device cpu: CPU backend ranks (launcher / exchange path), no GPU roof"}
     else:
-        st = R.stats(frame, seed=0, samples=(s0, s1 - s0))
-    px_launch = shard.tiles_per_rank * max(1, shard.chunks) * 64 if tiles_mode else W * H
-    bytes_launch = algorithmic_bytes(st, info, px_launch)
-    avg_ms = sum(kernel_ms) / len(kernel_ms)
-    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    pmc = load_pmc(args, args.config, pmc) if ws == 1 else None
-    roof = roofline(pmc, avg_ms)
-    roof["cache_served"] = {"bytes_per_launch": int(bytes_launch),
-                            "bytes_per_sample": round(bytes_launch / max(1, st["samples"]), 1),
-                            "gbs": round(achieved, 1)}
-    roof["counters"] = st
-    if st.get("cyc_loop"):
-        # STATS instance: shares of a wavefront's loop time per region (s_memtime)
-        roof["phase_share"] = {k[4:]: round(st[k] / st["cyc_loop"], 4) for k in (
-            "cyc_regen", "cyc_trace", "cyc_media", "cyc_shade", "cyc_lights")}
-    roof["lane_utilisation"] = {
-        "traversal": round(st["node_visits"] / max(1, 64 * st["wave_node_iters"]), 4),
-        "leaf": round((st["sphere_tests"] + st["quad_tests"]) / max(1, 64 * st["wave_leaf_iters"]), 4),
-        "shading": round(st["shade_events"] / max(1, 64 * st["wave_shade_iters"]), 4),
-        "path_trips": round(st["segments"] / max(1, 64 * st["wave_trips"]), 4)}
-    if st.get("wave_noise_iters"):
-        roof["lane_utilisation"]["noise_albedo"] = round(
-            st["noise_evals"] / (64 * st["wave_noise_iters"]), 4)
-    if st.get("medium_box_tests"):
-        # box-boundary media: share of their lanes box_span deferred to the
-        # general boundary scan (edge / corner / parallel rays)
-        roof["lane_utilisation"]["medium_box_deferred"] = round(
-            st["medium_box_deferred"] / st["medium_box_tests"], 6)
-    if st.get("model_trace_max"):
-        # the node-loop SIMD model (STATS): one walk per lane per trip vs each
-        # lane's walks of two consecutive trips back to back (two walks per lane)
-        roof["lane_utilisation"]["traversal_model_one_walk"] = round(
-            st["node_visits"] / (64 * st["model_trace_max"]), 4)
-        roof["lane_utilisation"]["traversal_model_two_walks"] = round(
-            st["node_visits"] / (64 * max(1, st["model_trace_pair_max"])), 4)
-    roof["note"] = ("fp64 vector roof (VALU-issue bound, scene LDS/cache resident); "
-                    "N>1 lines carry no PMC data (traffic null)"
-                    if ws == 1 else "N>1: no PMC pass in multi-rank runs (traffic null)")
+        roof = gpu_roofline(pmc)
 
     units_desc = ("library head/tail units, RT_CHUNKS_AUTO" if tiles_mode and shard.library_units
                   else "%d stratum chunks" % shard.chunks if tiles_mode else "")
@@ -816,6 +949,7 @@ def main():
         "value": round(value, 3),
         "unit": "Msamples/s",
         "n_gpus": ws,
+        "ranks_seen": seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
@@ -833,7 +967,9 @@ def main():
                                        "RCCL" if args.backend == "nccl" else "gloo")
                                    if tiles_mode else
                                    "stratum-shard x%d + %s reduce(sum)" % (
-                                       ws, "RCCL" if args.backend == "nccl" else "gloo"))},
+                                       ws, "RCCL" if args.backend == "nccl" else "gloo")),
+                   "device": "cpu backend (librtx_cpu.so)" if cpu else "gpu",
+                   "launcher": os.environ.get("RTX_BENCH_LAUNCHER", "torchrun" if use_pg else None)},
         "roofline": roof,
     }
     if check is not None:

@@ -24,19 +24,29 @@
 extern "C" {
 #endif
 
-#define RT_CPU_ABI_VERSION 1
+#define RT_CPU_ABI_VERSION 2
 
 int rt_cpu_abi_version(void);
 const char *rt_cpu_last_error(void); /* thread-local; valid until the next call */
 
 /* Render rows [row_begin,row_end) x strata [sample_begin, +sample_count) of
-   `frame` (from rt_camera_setup) on `threads` host threads (<= 0: one per
-   hardware thread) into host_rgb: row-major, 3 doubles per pixel, index
-   (j-row_begin)*W+i, RT_OUT_SCALED or RT_OUT_SUM.  Only whole-frame launches
-   (tile_first 0, tile_stride 0/1, RT_LAYOUT_FRAME, accumulate 0); tile
-   layouts are the GPU library's.  Synchronous. */
+   `frame` (from rt_camera_setup) on `threads` host threads (<= 0:
+   rt_cpu_default_threads()) into host_rgb, RT_OUT_SCALED or RT_OUT_SUM, in
+   the GPU library's output layouts (rt_render_params): RT_LAYOUT_FRAME,
+   row-major, 3 doubles per pixel, index (j-row_begin)*W+i; RT_LAYOUT_TILES,
+   the tiles tile_first + k*tile_stride of the band at [k][64][3], or with
+   strata_chunks > 1 each chunk's partial sums at [k][chunk][64][3].  The
+   params are validated as rt_render validates them (the same messages);
+   accumulate must be 0 and RT_CHUNKS_AUTO is refused (a GPU work-unit
+   plan).  A pixel's strata are added in stratum order, so any thread count
+   gives the same bytes.  Synchronous. */
 int rt_cpu_render(const rt_scene_desc *desc, const rt_frame *frame, const rt_render_params *params,
                   int32_t threads, double *host_rgb);
+
+/* The default thread count: the CPUs this process may run on (its affinity
+   mask, capped by a cgroup v2 cpu.max quota) -- not
+   std::thread::hardware_concurrency(), which counts the whole machine. */
+int rt_cpu_default_threads(void);
 
 #ifdef __cplusplus
 }

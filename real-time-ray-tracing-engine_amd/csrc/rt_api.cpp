@@ -116,89 +116,17 @@ struct DeviceGuard { // restore the caller's current device
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// the shared launch validation (rt_scene.cpp; the CPU backend applies the same)
 int to_device_camera(const rt_frame *f, DCamera &c) {
-  if (!f) return set_err(RT_ERR_INVALID, "null frame");
-  if (f->image_width < 1 || f->image_height < 1 || f->sqrt_spp < 1 || f->max_depth < 0)
-    return set_err(RT_ERR_INVALID, "invalid frame (width/height/sqrt_spp >= 1, max_depth >= 0)");
-  auto cp = [](double *d, const rt_vec3 &v) {
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-  };
-  cp(c.center, f->center);
-  cp(c.p00, f->pixel00_loc);
-  cp(c.du, f->pixel_delta_u);
-  cp(c.dv, f->pixel_delta_v);
-  cp(c.disk_u, f->defocus_disk_u);
-  cp(c.disk_v, f->defocus_disk_v);
-  cp(c.bg, f->background);
-  c.defocus_angle = f->defocus_angle;
-  c.scale = f->pixel_samples_scale;
-  c.W = f->image_width;
-  c.H = f->image_height;
-  c.sqrt_spp = f->sqrt_spp;
-  c.rs = 1.0 / c.sqrt_spp;
-  c.max_depth = f->max_depth;
-  return RT_OK;
+  std::string err;
+  int rc = rtx::device_camera(f, c, err);
+  return rc ? set_err(rc, err) : RT_OK;
 }
 
 int to_launch(const rt_frame *f, const rt_render_params *p, DLaunch &L) {
-  if (!p) return set_err(RT_ERR_INVALID, "null params");
-  int r0 = p->row_begin, r1 = p->row_end;
-  if (r0 == 0 && r1 == 0) r1 = f->image_height;
-  if (r0 < 0 || r1 > f->image_height || r1 <= r0)
-    return set_err(RT_ERR_INVALID, "row range outside the image");
-  int64_t nsamp = (int64_t)f->sqrt_spp * f->sqrt_spp;
-  int sb = p->sample_begin;
-  int64_t sc = p->sample_count < 0 ? nsamp - sb : p->sample_count;
-  if (sb < 0 || sc < 0 || sb + sc > nsamp)
-    return set_err(RT_ERR_INVALID, "sample range outside [0, sqrt_spp^2)");
-  if (64 * sc > 0x7FFFFFFF) return set_err(RT_ERR_UNSUPPORTED, "too many strata in one launch");
-  if ((int64_t)f->image_width * f->image_height > 0xFFFFFFFFll)
-    return set_err(RT_ERR_UNSUPPORTED, "image too large for 32-bit pixel keys");
-  if (p->output != RT_OUT_SCALED && p->output != RT_OUT_SUM)
-    return set_err(RT_ERR_INVALID, "unknown output mode");
-  L.row_begin = r0;
-  L.row_end = r1;
-  L.sample_begin = sb;
-  L.sample_count = (int32_t)sc;
-  L.seed_lo = (uint32_t)p->seed;
-  L.seed_hi = (uint32_t)(p->seed >> 32);
-  L.output = p->output;
-  L.accumulate = p->accumulate ? 1 : 0;
-  L.tiles_x = (f->image_width + 7) / 8;
-  L.tiles_y = (r1 - r0 + 7) / 8;
-  int stride = p->tile_stride <= 0 ? 1 : p->tile_stride;
-  if (p->tile_first < 0 || p->tile_first >= stride)
-    return set_err(RT_ERR_INVALID, "tile_first must be in [0, tile_stride)");
-  if (p->layout != RT_LAYOUT_FRAME && p->layout != RT_LAYOUT_TILES)
-    return set_err(RT_ERR_INVALID, "unknown output layout");
-  const int64_t n_tiles = (int64_t)L.tiles_x * L.tiles_y;
-  L.tile_first = p->tile_first;
-  L.tile_stride = stride;
-  L.n_local_tiles = (int32_t)(n_tiles > p->tile_first ? (n_tiles - p->tile_first + stride - 1) / stride : 0);
-  L.compact = p->layout == RT_LAYOUT_TILES;
-  int chunks = p->strata_chunks <= 0 ? 1 : p->strata_chunks;
-  if (chunks > 1 && !L.compact)
-    return set_err(RT_ERR_INVALID, "strata_chunks > 1 needs RT_LAYOUT_TILES");
-  if (chunks > L.sample_count && L.sample_count > 0)
-    return set_err(RT_ERR_INVALID, "strata_chunks exceeds the launched strata");
-  if ((int64_t)L.n_local_tiles * chunks > 0x7FFFFFFF)
-    return set_err(RT_ERR_UNSUPPORTED, "too many work units");
-  L.n_chunks = chunks;
-  L.chunk_strata = (L.sample_count + chunks - 1) / chunks;
-  L.unit_ctr = nullptr;
-  L.grid_cap = 0;
-  L.tile_order = nullptr;
-  L.tile_cost = nullptr;
-  // one chunk: every tile is a whole unit; strata_chunks > 1 (tile layout):
-  // every tile split, its chunk partials are the caller's output (the launcher
-  // points parts at the output buffer)
-  L.n_head = chunks > 1 ? 0 : L.n_local_tiles;
-  L.head_chunks = 1;
-  L.parts = nullptr;
-  L.parts_final = chunks > 1 ? 1 : 0;
-  return RT_OK;
+  std::string err;
+  int rc = rtx::launch_geometry(f, p, L, err);
+  return rc ? set_err(rc, err) : RT_OK;
 }
 
 // doubles an output of this launch covers

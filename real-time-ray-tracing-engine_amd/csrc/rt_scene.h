@@ -101,5 +101,14 @@ int compile_scene(const rt_scene_desc *desc, HostScene &out, std::string &err);
 // Camera::initialize (Camera.cpp:31-73), same operation order.
 int camera_setup(const rt_camera_desc *cam, rt_frame *frame, std::string &err);
 
+// The validation both backends apply to a launch (librtx_hip.so's rt_render*
+// and librtx_cpu.so's rt_cpu_render): a set-up frame -> the kernel's camera
+// values, and the params' row band, stratum range, output, layout, tile subset
+// and chunk count -> the launch geometry (one work unit per tile, or every
+// tile in strata_chunks chunks).  strata_chunks < 0 is refused here:
+// RT_CHUNKS_AUTO is resolved by the callers that accept it.
+int device_camera(const rt_frame *frame, DCamera &c, std::string &err);
+int launch_geometry(const rt_frame *frame, const rt_render_params *p, DLaunch &L, std::string &err);
+
 } // namespace rtx
 #endif

@@ -16,6 +16,10 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <utility>
@@ -65,28 +69,25 @@ constexpr std::array<PixelFn, sizeof...(Fs)> pixel_fns(std::integer_sequence<uns
 // the binary-walk instances: MEDIA | XFORM | LIGHTS | NOISE | FLAT
 constexpr auto kPixelFns = pixel_fns(std::make_integer_sequence<unsigned, F_FLAT * 2>{});
 
-DCamera host_camera(const rt_frame &f) {
-  DCamera C{};
-  auto cp = [](double *d, const rt_vec3 &v) {
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-  };
-  cp(C.center, f.center);
-  cp(C.p00, f.pixel00_loc);
-  cp(C.du, f.pixel_delta_u);
-  cp(C.dv, f.pixel_delta_v);
-  cp(C.disk_u, f.defocus_disk_u);
-  cp(C.disk_v, f.defocus_disk_v);
-  cp(C.bg, f.background);
-  C.defocus_angle = f.defocus_angle;
-  C.scale = f.pixel_samples_scale;
-  C.W = f.image_width;
-  C.H = f.image_height;
-  C.sqrt_spp = f.sqrt_spp;
-  C.rs = 1.0 / f.sqrt_spp;
-  C.max_depth = f.max_depth;
-  return C;
+// Default worker count: the CPUs this process may run on -- the affinity
+// mask, capped by a cgroup v2 cpu.max quota -- not hardware_concurrency(),
+// which on a quota-limited box (the GPU box: 16 of 256) oversubscribes the
+// quota many times over (README: the reference's pool collapsing there).
+int usable_cpus() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  if (FILE *fp = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long per = 0;
+    if (std::fscanf(fp, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+      const long long quota = std::atoll(q);
+      if (quota > 0) n = std::min<int>(n, (int)std::max<long long>(1, quota / per));
+    }
+    std::fclose(fp);
+  }
+  return std::max(1, n);
 }
 
 } // namespace
@@ -97,25 +98,23 @@ int rt_cpu_abi_version(void) { return RT_CPU_ABI_VERSION; }
 
 const char *rt_cpu_last_error(void) { return g_err.c_str(); }
 
+int rt_cpu_default_threads(void) { return usable_cpus(); }
+
 int rt_cpu_render(const rt_scene_desc *desc, const rt_frame *f, const rt_render_params *p,
                   int32_t threads, double *host_rgb) {
-  if (!desc || !f || !p || !host_rgb) return fail(RT_ERR_INVALID, "null argument");
-  if (f->image_width <= 0 || f->image_height <= 0 || f->sqrt_spp <= 0)
-    return fail(RT_ERR_INVALID, "frame not set up (rt_camera_setup)");
-  if (p->tile_first != 0 || p->tile_stride > 1 || p->layout != RT_LAYOUT_FRAME || p->accumulate)
-    return fail(RT_ERR_INVALID, "rt_cpu_render takes whole-frame launches (RT_LAYOUT_FRAME, "
-                                "tile_first 0, tile_stride 0/1, accumulate 0)");
-  if (p->output != RT_OUT_SCALED && p->output != RT_OUT_SUM) return fail(RT_ERR_INVALID, "unknown output mode");
-  int r0 = p->row_begin, r1 = p->row_end;
-  if (r0 == 0 && r1 == 0) r1 = f->image_height;
-  if (r0 < 0 || r1 > f->image_height || r0 > r1) return fail(RT_ERR_INVALID, "row range outside the image");
-  const int n = f->sqrt_spp * f->sqrt_spp;
-  const int s0 = p->sample_begin, s1 = p->sample_count < 0 ? n : s0 + p->sample_count;
-  if (s0 < 0 || s1 < s0 || s1 > n) return fail(RT_ERR_INVALID, "sample range outside [0, sqrt_spp^2)");
+  if (!desc || !host_rgb) return fail(RT_ERR_INVALID, "null argument");
+  // the GPU library's validation (rt_scene.cpp launch_geometry), so both
+  // backends accept and refuse the same launches
+  DCamera C;
+  DLaunch L;
+  std::string err;
+  int rc = rtx::device_camera(f, C, err);
+  if (rc == RT_OK) rc = rtx::launch_geometry(f, p, L, err);
+  if (rc != RT_OK) return fail(rc, err);
+  if (L.accumulate) return fail(RT_ERR_INVALID, "rt_cpu_render writes its output (accumulate 0)");
 
   rtx::HostScene H;
-  std::string err;
-  int rc = rtx::compile_scene(desc, H, err);
+  rc = rtx::compile_scene(desc, H, err);
   if (rc != RT_OK) return fail(rc, err);
   if (H.device_bvh) rtx::build_world_bvh_host(H); // the device builders are the GPU library's
   const int stack_depth = std::max(1, H.bvh_depth + 1);
@@ -152,23 +151,56 @@ int rt_cpu_render(const rt_scene_desc *desc, const rt_frame *f, const rt_render_
     for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, RT_SLAB_FMA && RT_SLAB_SIGN));
     lnodes = (const DNode *)(const void *)lnodes_l.data();
   }
-  const DCamera C = host_camera(*f);
   const PixelFn fn = kPixelFns[S.features & (F_FLAT * 2 - 1)];
-  const bool scaled = p->output == RT_OUT_SCALED;
+  const bool scaled = L.output == RT_OUT_SCALED;
   const uint64_t seed = p->seed;
+  const int s0 = L.sample_begin, s1 = L.sample_begin + L.sample_count;
 
-  int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
-  nt = std::max(1, std::min(nt, std::max(1, r1 - r0)));
-  std::atomic<int> next_row{r0};
+  // Work items: frame layout -- rows of the band, pixels (j - row_begin) * W + i;
+  // tile layout -- the launch's tiles t = tile_first + k * tile_stride (8x8,
+  // row-major over the band), tile k's pixel s = (j - y0) * 8 + (i - x0) at
+  // [k][s] (one chunk) or each chunk's partial sums at [k][c][s], chunk c the
+  // strata [s0 + c * chunk_strata, +chunk_strata) -- the GPU library's
+  // RT_LAYOUT_TILES output; pixels past the frame's edge are 0.
+  const int n_items = L.compact ? L.n_local_tiles : L.row_end - L.row_begin;
+  int nt = threads > 0 ? threads : usable_cpus();
+  nt = std::max(1, std::min(nt, std::max(1, n_items)));
+  std::atomic<int> next{0};
+  std::atomic<int> status{RT_OK};
   auto work = [&]() {
-    std::vector<int> stack((size_t)RT_STACK_DEPTH * 64);
-    for (int j; (j = next_row.fetch_add(1)) < r1;)
-      for (int i = 0; i < C.W; ++i) {
-        double acc[3] = {0.0, 0.0, 0.0};
-        fn(S, C, seed, i, j, s0, s1, stack.data(), lnodes, acc);
-        double *o = host_rgb + 3 * ((size_t)(j - r0) * C.W + i);
-        for (int c = 0; c < 3; ++c) o[c] = scaled ? C.scale * acc[c] : acc[c];
+    try {
+      std::vector<int> stack((size_t)RT_STACK_DEPTH * 64);
+      for (int k; status.load(std::memory_order_relaxed) == RT_OK && (k = next.fetch_add(1)) < n_items;) {
+        if (!L.compact) {
+          const int j = L.row_begin + k;
+          for (int i = 0; i < C.W; ++i) {
+            double acc[3] = {0.0, 0.0, 0.0};
+            fn(S, C, seed, i, j, s0, s1, stack.data(), lnodes, acc);
+            double *o = host_rgb + 3 * ((size_t)k * C.W + i);
+            for (int c = 0; c < 3; ++c) o[c] = scaled ? C.scale * acc[c] : acc[c];
+          }
+          continue;
+        }
+        const int64_t t = L.tile_first + (int64_t)k * L.tile_stride;
+        const int x0 = (int)(t % L.tiles_x) * 8, y0 = L.row_begin + (int)(t / L.tiles_x) * 8;
+        for (int c = 0; c < L.n_chunks; ++c) {
+          const int c0 = std::min(s1, s0 + c * L.chunk_strata), c1 = std::min(s1, c0 + L.chunk_strata);
+          double *o = host_rgb + ((size_t)k * L.n_chunks + c) * 64 * 3;
+          for (int sp = 0; sp < 64; ++sp) {
+            const int i = x0 + (sp & 7), j = y0 + (sp >> 3);
+            double acc[3] = {0.0, 0.0, 0.0};
+            if (i < C.W && j < L.row_end) fn(S, C, seed, i, j, c0, c1, stack.data(), lnodes, acc);
+            for (int ch = 0; ch < 3; ++ch) o[3 * sp + ch] = scaled ? C.scale * acc[ch] : acc[ch];
+          }
+        }
       }
+    } catch (const std::bad_alloc &) {
+      int ok = RT_OK;
+      status.compare_exchange_strong(ok, RT_ERR_OOM);
+    } catch (...) {
+      int ok = RT_OK;
+      status.compare_exchange_strong(ok, RT_ERR_INVALID);
+    }
   };
   std::vector<std::thread> pool;
   try {
@@ -178,6 +210,9 @@ int rt_cpu_render(const rt_scene_desc *desc, const rt_frame *f, const rt_render_
   }
   work();
   for (auto &t : pool) t.join();
+  const int st = status.load();
+  if (st == RT_ERR_OOM) return fail(st, "out of host memory in a render thread");
+  if (st != RT_OK) return fail(st, "a render thread threw");
   return RT_OK;
 }
 

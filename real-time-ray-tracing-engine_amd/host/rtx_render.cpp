@@ -18,8 +18,9 @@
 //                     path; here that is --backend cpu.
 //   --backend cpu     the CPU backend (librtx_cpu.so, include/rt_cpu.h): the
 //                     kernel's per-path source compiled for the host, image rows
-//                     on --threads N host threads (default: one per hardware
-//                     thread; StaticCamera::render_cpu's ThreadPool role,
+//                     on --threads N host threads (default: the CPUs this
+//                     process may use -- affinity mask and cgroup quota,
+//                     rt_cpu_default_threads; StaticCamera::render_cpu's ThreadPool role,
 //                     StaticCamera.cpp:32-134).  Chosen, never a fallback: the
 //                     default backend fails if the GPU library cannot render.
 //   -b                scene use_bvh (the reference's light-list BVH split); the
@@ -68,7 +69,7 @@ struct Options {
   int device = 0;
   int gpus = 1, shards = 0;
   bool cpu = false; // --backend cpu
-  int threads = 0;  // --threads (CPU backend); 0: one per hardware thread
+  int threads = 0;  // --threads (CPU backend); 0: rt_cpu_default_threads()
 };
 
 bool parse_int(const char *s, int &out) {
@@ -201,7 +202,7 @@ void print_help() {
          "  --gpus <int>               Devices to render on, from --device (default: 1)\n"
          "  --shards <int>             Tile shards over those devices (default: --gpus)\n"
          "  --backend <hip|cpu>        GPU library (default) or the CPU backend\n"
-         "  --threads <int>            CPU backend threads (default: one per hardware thread)\n"
+         "  --threads <int>            CPU backend threads (default: the CPUs this process may use)\n"
          "  --dump-desc                Print the flattened scene description and exit\n";
 }
 
@@ -441,7 +442,8 @@ int main(int argc, char **argv) {
   release();
   std::clog << "\rDone. " << W << "x" << H << " @ " << n_strata << " spp, "
             << (double)W * H * n_strata / secs / 1e6 << " Msamples/s";
-  if (opt.cpu) std::clog << " (CPU backend)";
+  if (opt.cpu)
+    std::clog << " (CPU backend, " << (opt.threads > 0 ? opt.threads : rt_cpu_default_threads()) << " threads)";
   else if (shards > 1) std::clog << " (" << shards << " tile shards on " << opt.gpus << " device(s))";
   std::clog << "\n";
 

@@ -123,6 +123,29 @@ def device_tiles_to_frame(gathered, frame, out):
     return out
 
 
+def host_tiles_sum(parts, out):
+    """rt_tiles_sum_device's operation on host tensors (the CPU backend's
+    ranks): chunk partials added in chunk order, sequentially."""
+    acc = parts[:, 0].clone()
+    for c in range(1, parts.shape[1]):
+        acc = acc + parts[:, c]
+    out.copy_(acc)
+    return out
+
+
+def host_tiles_to_frame(gathered, frame, out):
+    """rt_tiles_to_frame_device's reorder on host tensors (the CPU backend's
+    ranks): gathered [world, T_r, 64, 3], rank r holding tiles r, r + world,
+    ... -> the frame's raw sums out [H, W, 3]."""
+    world, t_r = gathered.shape[0], gathered.shape[1]
+    W, H = frame.image_width, frame.image_height
+    tx, ty = (W + 7) // 8, (H + 7) // 8
+    flat = gathered.transpose(0, 1).reshape(t_r * world, 64, gathered.shape[-1])[:tx * ty]
+    img = flat.reshape(ty, tx, 8, 8, -1).permute(0, 2, 1, 3, 4).reshape(ty * 8, tx * 8, -1)
+    out.copy_(img[:H, :W])
+    return out
+
+
 def shard_units(strata):
     """Work-unit target of one rank: 32768 units (8 per wave slot) at 64 strata
     per pixel, growing with sqrt(strata / 64) up to 4x -- the fastest of the
@@ -175,6 +198,11 @@ class TileShardedRenderer:
         self.tiles_sum = tiles_sum or device_tiles_sum
         self.to_frame = to_frame or device_tiles_to_frame
 
+    def on_host(self):
+        """The host reorder and chunk sum (ranks on the CPU backend)."""
+        self.tiles_sum, self.to_frame = host_tiles_sum, host_tiles_to_frame
+        return self
+
     def buffer(self, device=None):
         if self.library_units:  # the tile sums themselves
             return self.sum_buffer(device)
@@ -220,6 +248,19 @@ class TileShardedRenderer:
         tiles = self.render(buf, seed)
         self.gather(tiles, gathered)
         return self.frame_sums(gathered) if self.rank == 0 else None
+
+
+def ranks_seen(device=None):
+    """Distinct rank ids the default process group's collective actually
+    reached (an all_gather of every rank's id): the world the exchange ran
+    over, as opposed to the world the launcher meant to start."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    ws = dist.get_world_size()
+    mine = torch.tensor([dist.get_rank()], dtype=torch.int64, device=device)
+    allv = [torch.zeros_like(mine) for _ in range(ws)]
+    dist.all_gather(allv, mine)
+    return len({int(v.item()) for v in allv})
 
 
 def max_over_ranks(value, device=None):

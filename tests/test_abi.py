@@ -28,7 +28,8 @@ def test_cpu_backend_header_symbols_are_exported():
     cpu_h = os.path.join(O.ROOT, "include", "rt_cpu.h")
     lib = os.path.join(os.path.dirname(LIB_PATH), "librtx_cpu.so")
     declared = header_functions(cpu_h)
-    assert declared == ["rt_cpu_abi_version", "rt_cpu_last_error", "rt_cpu_render"]
+    assert declared == ["rt_cpu_abi_version", "rt_cpu_default_threads", "rt_cpu_last_error",
+                        "rt_cpu_render"]
     L = C.CDLL(lib)
     for name in declared:
         assert hasattr(L, name), name

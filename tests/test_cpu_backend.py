@@ -32,7 +32,7 @@ def cpu():
     L.rt_cpu_render.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.Frame),
                                 C.POINTER(abi.RenderParams), C.c_int32, C.POINTER(C.c_double)]
     L.rt_cpu_last_error.restype = C.c_char_p
-    assert L.rt_cpu_abi_version() == 1
+    assert L.rt_cpu_abi_version() == 2
     return L
 
 
@@ -81,14 +81,104 @@ def test_cpu_backend_threads_rows_and_strata(cpu):
     np.testing.assert_allclose(a + b, one, rtol=1e-13, atol=1e-13)
 
 
-def test_cpu_backend_refuses_tile_launches(cpu):
+def _tiles_of(img, first, stride, r0=0):
+    """RT_LAYOUT_TILES extraction of a frame-layout band (tiles numbered from
+    row r0; pixels past the edge 0)."""
+    H, W, _ = img.shape
+    tx, ty = (W + 7) // 8, (H + 7) // 8
+    out = []
+    for t in range(first, tx * ty, stride):
+        x0, y0 = (t % tx) * 8, (t // tx) * 8
+        tile = np.zeros((64, 3))
+        for s in range(64):
+            i, j = x0 + (s & 7), y0 + (s >> 3)
+            if i < W and j < H:
+                tile[s] = img[j, i]
+        out.append(tile)
+    return np.array(out).reshape(-1, 64, 3)
+
+
+def test_cpu_backend_tile_layout(cpu):
+    """RT_LAYOUT_TILES (the GPU library's tile-shard output, rtx/dist.py): the
+    tiles tile_first + k * tile_stride of a ragged frame are the frame's pixels
+    bit for bit (0 past the edge); with strata_chunks each chunk's partial
+    sums, chunk c the strata [c * ceil(n / chunks), ...), adding up to the
+    tile sums; a row band numbers its tiles from its first row."""
+    S = load_scene(os.path.join(SCENES, "cornell.json"))
+    f = camera_frame(S.camera_desc(image_width=27, samples_per_pixel=9, max_depth=5))
+    _, full = _render(cpu, S, f, 6, threads=3, output=abi.RT_OUT_SUM)
+    n_tiles = ((f.image_width + 7) // 8) * ((f.image_height + 7) // 8)
+    for first, stride in ((0, 1), (1, 3), (2, 3)):
+        n = (n_tiles - first + stride - 1) // stride
+        p = abi.RenderParams()
+        p.seed, p.output, p.layout = 6, abi.RT_OUT_SUM, abi.RT_LAYOUT_TILES
+        p.sample_count, p.tile_first, p.tile_stride = -1, first, stride
+        out = np.full((n, 64, 3), np.nan)
+        d = S.desc()
+        assert cpu.rt_cpu_render(C.byref(d), C.byref(f), C.byref(p), 2,
+                                 out.ctypes.data_as(C.POINTER(C.c_double))) == 0
+        assert np.array_equal(out, _tiles_of(full, first, stride)), (first, stride)
+        p.strata_chunks = 4  # 9 strata -> chunks of 3, 3, 3, 0
+        parts = np.full((n, 4, 64, 3), np.nan)
+        assert cpu.rt_cpu_render(C.byref(d), C.byref(f), C.byref(p), 2,
+                                 parts.ctypes.data_as(C.POINTER(C.c_double))) == 0
+        assert not parts[:, 3].any()
+        np.testing.assert_allclose(parts.sum(axis=1), out, rtol=1e-13, atol=1e-13)
+        _, c0 = _render(cpu, S, f, 6, samples=(0, 3), output=abi.RT_OUT_SUM)
+        assert np.array_equal(parts[:, 0], _tiles_of(c0, first, stride))
+    # a row band: tiles of rows [5, 20)
+    p = abi.RenderParams()
+    p.seed, p.output, p.layout, p.sample_count = 6, abi.RT_OUT_SUM, abi.RT_LAYOUT_TILES, -1
+    p.row_begin, p.row_end = 5, 20
+    nb = ((f.image_width + 7) // 8) * 2
+    band = np.zeros((nb, 64, 3))
+    d = S.desc()
+    assert cpu.rt_cpu_render(C.byref(d), C.byref(f), C.byref(p), 1,
+                             band.ctypes.data_as(C.POINTER(C.c_double))) == 0
+    assert np.array_equal(band, _tiles_of(full[5:20], 0, 1))
+
+
+def test_cpu_backend_validates_like_the_gpu_library(cpu):
+    """The launch validation is the GPU library's (rt_scene.cpp launch_geometry):
+    the same refusals and messages; accumulate and RT_CHUNKS_AUTO (a GPU
+    work-unit plan) are refused."""
     S = load_scene(os.path.join(SCENES, "three_spheres.json"))
     f = camera_frame(S.camera_desc(image_width=16, samples_per_pixel=4, max_depth=4))
-    for kw in ({"layout": abi.RT_LAYOUT_TILES}, {"tile_stride": 2}, {"accumulate": 1}):
+    for kw, msg in (({"accumulate": 1}, b"accumulate"),
+                    ({"strata_chunks": abi.RT_CHUNKS_AUTO, "layout": abi.RT_LAYOUT_TILES}, b"RT_CHUNKS_AUTO"),
+                    ({"strata_chunks": 2}, b"needs RT_LAYOUT_TILES"),
+                    ({"tile_first": 2, "tile_stride": 2}, b"tile_first"),
+                    ({"layout": 7}, b"layout"),
+                    ({"output": 9}, b"output")):
         rc, _ = _render(cpu, S, f, 1, **kw)
-        assert rc == abi.RT_ERR_INVALID, kw
+        assert rc == abi.RT_ERR_INVALID and msg in cpu.rt_cpu_last_error(), kw
     rc, _ = _render(cpu, S, f, 1, samples=(3, 5))  # past sqrt_spp^2 = 4
-    assert rc == abi.RT_ERR_INVALID
+    assert rc == abi.RT_ERR_INVALID and b"sample range" in cpu.rt_cpu_last_error()
+    rc, _ = _render(cpu, S, f, 1, rows=(4, f.image_height + 1))
+    assert rc == abi.RT_ERR_INVALID and b"row range" in cpu.rt_cpu_last_error()
+    bad = abi.Frame()
+    C.memmove(C.byref(bad), C.byref(f), C.sizeof(f))
+    bad.max_depth = -1
+    p = abi.RenderParams()
+    out = np.zeros((f.image_height, f.image_width, 3))
+    d = S.desc()
+    assert cpu.rt_cpu_render(C.byref(d), C.byref(bad), C.byref(p), 1,
+                             out.ctypes.data_as(C.POINTER(C.c_double))) == abi.RT_ERR_INVALID
+    assert b"max_depth" in cpu.rt_cpu_last_error()
+
+
+def test_cpu_backend_default_threads_follow_the_quota(cpu):
+    """rt_cpu_default_threads: the CPUs this process may use (affinity mask,
+    cgroup cpu.max quota), not the machine's hardware_concurrency()."""
+    n = cpu.rt_cpu_default_threads()
+    want = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            want = min(want, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    assert n == want >= 1
 
 
 @pytest.mark.skipif(not os.path.exists(CLI), reason="build/rtx_render not built")

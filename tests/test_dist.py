@@ -136,6 +136,25 @@ def test_tiles_to_frame_reorders_ragged_frames():
         assert np.array_equal(got, img)
 
 
+def test_host_exchange_ops_match_the_references():
+    """rtx.dist's host chunk sum and tile -> frame reorder (the CPU backend's
+    ranks, bench.py --device cpu) equal the references above bit for bit."""
+    from rtx.dist import host_tiles_sum, host_tiles_to_frame
+    from rtx.render import camera_frame
+    g = torch.Generator().manual_seed(3)
+    S = load_scene(SCENE)
+    for width, world, chunks in [(27, 3, 5), (16, 1, 1), (40, 4, 2)]:
+        f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=4, max_depth=6))
+        n, t_r = tile_counts(f, world)
+        parts = torch.randn((t_r, chunks, 64, 3), generator=g, dtype=torch.float64)
+        want = tiles_sum(parts, torch.empty((t_r, 64, 3), dtype=torch.float64))
+        assert torch.equal(host_tiles_sum(parts, torch.empty_like(want)), want)
+        gath = torch.randn((world, t_r, 64, 3), generator=g, dtype=torch.float64)
+        out = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64)
+        assert torch.equal(host_tiles_to_frame(gath, f, out),
+                           tiles_to_frame(gath, f.image_width, f.image_height))
+
+
 def test_shard_chunks_follow_the_strata():
     """8-way tile shards: the work-unit target grows with the strata per pixel
     (profiles/r04q_shard_units_*.log, r04v_shard_units_*.log) and the chunk

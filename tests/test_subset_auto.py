@@ -84,6 +84,15 @@ def test_auto_needs_tile_layout_and_raw_sums():
             args.update(kw)
             with pytest.raises(RtError):
                 R.render_device(f, buf.data_ptr(), 0, **args)
+        # rt_render and a frame-layout rt_render_stats refuse it too (ADVICE r5:
+        # they used to run a one-chunk launch silently)
+        for layout in (abi.RT_LAYOUT_FRAME, abi.RT_LAYOUT_TILES):
+            with pytest.raises(RtError, match="RT_CHUNKS_AUTO"):
+                R.render(f, seed=1, output=abi.RT_OUT_SUM, layout=layout, chunks=abi.RT_CHUNKS_AUTO)
+        with pytest.raises(RtError, match="RT_CHUNKS_AUTO"):
+            R.stats(f, seed=1, chunks=abi.RT_CHUNKS_AUTO)
+        with pytest.raises(RtError, match="strata_chunks"):
+            R.render(f, seed=1, output=abi.RT_OUT_SUM, layout=abi.RT_LAYOUT_TILES, chunks=-3)
 
 
 def test_auto_edge_subsets():
