@@ -87,6 +87,10 @@ struct rt_scene {
   int order_cap = 0, order_cur = 0;
   bool order_ready = false;
   int32_t order_sig[10] = {};
+  // caller streams rt_render_device launched on, each with an event recorded
+  // after the scene's last work there (note_stream): destroy and buffer growth
+  // wait on these and on the scene's own stream -- not on the whole device
+  std::vector<std::pair<hipStream_t, hipEvent_t>> used;
 };
 
 namespace {
@@ -115,6 +119,55 @@ struct DeviceGuard { // restore the caller's current device
 };
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Scene memory is stream-ordered: hipMallocAsync / hipFreeAsync on the scene's
+// own stream.  A plain hipFree -- and hipFreeAsync of hipMalloc'd memory --
+// waits for every stream of the device (tools/free_probe.hip on gfx950: 300 ms
+// behind another stream's 300 ms kernel); hipFreeAsync of pool memory returns
+// at once.  So destroying or growing one scene waits only for that scene's own
+// work (wait_scene), never for other scenes or threads on the device.
+hipError_t scene_alloc(rt_scene *s, void **p, size_t bytes) {
+  *p = nullptr;
+  hipError_t e = hipMallocAsync(p, std::max<size_t>(bytes, 1), s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream); // usable from any stream from here on
+  if (e != hipSuccess) *p = nullptr;
+  return e;
+}
+template <class T>
+void scene_free(rt_scene *s, T *&p) { // after wait_scene: nothing still reads p
+  if (p) (void)hipFreeAsync((void *)p, s->stream);
+  p = nullptr;
+}
+hipError_t upload(rt_scene *s, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s->stream);
+  return e == hipSuccess ? hipStreamSynchronize(s->stream) : e;
+}
+// everything this scene has launched has completed: its own stream, and its
+// last launch on every caller stream
+void wait_scene(rt_scene *s) {
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (auto &u : s->used) (void)hipEventSynchronize(u.second);
+}
+// after rt_render_device's work on caller stream st
+int note_stream(rt_scene *s, hipStream_t st) {
+  if (st == s->stream) return RT_OK;
+  auto it = std::find_if(s->used.begin(), s->used.end(), [&](const auto &u) { return u.first == st; });
+  if (it == s->used.end()) {
+    constexpr size_t kMaxStreams = 64; // a bound: the oldest stream's work is waited for and dropped
+    if (s->used.size() >= kMaxStreams) {
+      (void)hipEventSynchronize(s->used.front().second);
+      (void)hipEventDestroy(s->used.front().second);
+      s->used.erase(s->used.begin());
+    }
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_err(e, "hipEventCreate");
+    s->used.emplace_back(st, ev);
+    it = s->used.end() - 1;
+  }
+  hipError_t e = hipEventRecord(it->second, st);
+  return e == hipSuccess ? RT_OK : hip_err(e, "hipEventRecord");
+}
 
 // the shared launch validation (rt_scene.cpp; the CPU backend applies the same)
 int to_device_camera(const rt_frame *f, DCamera &c) {
@@ -184,7 +237,7 @@ static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *
   const size_t lb = sah ? rtk_sah_temp_bytes(n) : rtk_lbvh_temp_bytes(n);
   const size_t total = a_box + a_items + 256 + lb;
   char *tmp = nullptr;
-  hipError_t e = hipMalloc((void **)&tmp, total);
+  hipError_t e = scene_alloc(s, (void **)&tmp, total);
   if (e != hipSuccess) return e;
   double *d_box = (double *)tmp;
   DItem *d_sorted = (DItem *)(tmp + a_box);
@@ -207,7 +260,8 @@ static hipError_t device_bvh_build(rt_scene *s, const rtx::HostScene &H, DNode *
   if (e == hipSuccess)
     e = hipMemcpyAsync(items, d_sorted, sizeof(DItem) * n, hipMemcpyDeviceToDevice, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
-  (void)hipFree(tmp);
+  if (e != hipSuccess) (void)hipStreamSynchronize(s->stream); // nothing may still use tmp
+  scene_free(s, tmp);
   return e;
 }
 
@@ -280,26 +334,24 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
   s->device = device;
   s->tune = tune;
   s->block_bytes = off;
-  e = hipMalloc((void **)&s->block, off);
+  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess) {
+    rt_scene_destroy(s);
+    return hip_err(e, "stream/event create");
+  }
+  e = scene_alloc(s, (void **)&s->block, off);
   if (e != hipSuccess) {
-    delete s;
-    return set_err(RT_ERR_OOM, std::string("hipMalloc scene: ") + hipGetErrorString(e));
+    rt_scene_destroy(s);
+    return set_err(RT_ERR_OOM, std::string("hipMallocAsync scene: ") + hipGetErrorString(e));
   }
   for (const Part &p : parts)
     if (p.src && p.bytes) {
-      e = hipMemcpy(s->block + p.off, p.src, p.bytes, hipMemcpyHostToDevice);
+      e = upload(s, s->block + p.off, p.src, p.bytes, hipMemcpyHostToDevice);
       if (e != hipSuccess) {
-        (void)hipFree(s->block);
-        delete s;
-        return hip_err(e, "hipMemcpy scene");
+        rt_scene_destroy(s);
+        return hip_err(e, "upload scene");
       }
     }
-  if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess) {
-    (void)hipFree(s->block);
-    delete s;
-    return hip_err(e, "stream/event create");
-  }
   auto P = [&](size_t i) { return (const void *)(s->block + parts[i].off); };
   // with H.nodes holding the final binary tree: collapse and upload the 4-wide
   // one -- kept binary when its stack would not fit RT_STACK_DEPTH4, or when
@@ -320,8 +372,8 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
     s->binary_cost = rtx::bvh_sah_cost(H.nodes);
     H.bvh_arity = 4;
     H.bvh_depth4 = d4;
-    return hipMemcpy((void *)P(iN), H.nodes4.data(), H.nodes4.size() * sizeof(DNode4),
-                     hipMemcpyHostToDevice);
+    return upload(s, (void *)P(iN), H.nodes4.data(), H.nodes4.size() * sizeof(DNode4),
+                  hipMemcpyHostToDevice);
   };
   DScene &d = s->ds;
   d.nodes = (const DNode *)P(iN);
@@ -363,8 +415,8 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
       H.n_root_items = tree.root_leaf;
       builder = H.device_bvh;
       if (want4 && !H.root_is_leaf) { // the collapse runs on the host copy
-        hipError_t ce = hipMemcpy(H.nodes.data(), P(iN), H.nodes.size() * sizeof(DNode),
-                                  hipMemcpyDeviceToHost);
+        hipError_t ce = upload(s, H.nodes.data(), P(iN), H.nodes.size() * sizeof(DNode),
+                               hipMemcpyDeviceToHost);
         if (ce != hipSuccess) {
           rt_scene_destroy(s);
           return hip_err(ce, "BVH download");
@@ -372,11 +424,11 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
       }
     } else { // too deep for the per-lane stack: rebuild on the host (depth-capped SAH)
       rtx::build_world_bvh_host(H);
-      hipError_t ue = hipMemcpy((void *)P(iN), H.nodes.data(), H.nodes.size() * sizeof(DNode),
-                                hipMemcpyHostToDevice);
+      hipError_t ue = upload(s, (void *)P(iN), H.nodes.data(), H.nodes.size() * sizeof(DNode),
+                             hipMemcpyHostToDevice);
       if (ue == hipSuccess)
-        ue = hipMemcpy((void *)P(iI), H.items.data(), H.items.size() * sizeof(DItem),
-                       hipMemcpyHostToDevice);
+        ue = upload(s, (void *)P(iI), H.items.data(), H.items.size() * sizeof(DItem),
+                    hipMemcpyHostToDevice);
       if (ue != hipSuccess) {
         rt_scene_destroy(s);
         return hip_err(ue, "BVH upload");
@@ -512,14 +564,20 @@ int rt_scene_destroy(rt_scene *s) {
   if (!s) return RT_OK;
   DeviceGuard g(s->device);
   // launches on caller streams (rt_render_device) may still read the scene's
-  // tables and use its scratch / tile-order buffers: wait for the device
-  (void)hipDeviceSynchronize();
-  if (s->out_buf) (void)hipFree(s->out_buf);
-  if (s->scratch) (void)hipFree(s->scratch);
-  if (s->tile_cost) (void)hipFree(s->tile_cost);
-  if (s->tile_order[0]) (void)hipFree(s->tile_order[0]);
-  if (s->tile_order[1]) (void)hipFree(s->tile_order[1]);
-  if (s->block) (void)hipFree(s->block);
+  // tables and use its scratch / tile-order buffers: wait for this scene's
+  // work -- its stream and its last launch on each caller stream -- and no
+  // other (stream-ordered frees, scene_alloc)
+  wait_scene(s);
+  if (s->stream) {
+    scene_free(s, s->out_buf);
+    scene_free(s, s->scratch);
+    scene_free(s, s->tile_cost);
+    scene_free(s, s->tile_order[0]);
+    scene_free(s, s->tile_order[1]);
+    scene_free(s, s->block);
+    (void)hipStreamSynchronize(s->stream);
+  }
+  for (auto &u : s->used) (void)hipEventDestroy(u.second);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -665,13 +723,12 @@ static SplitPlan subset_plan(const rt_scene *s, const DLaunch &L) {
 static int ensure_scratch(rt_scene *s, size_t bytes) {
   if (s->scratch_bytes >= bytes) return RT_OK;
   if (s->scratch) {
-    (void)hipDeviceSynchronize(); // a launch on any stream may still read it
-    (void)hipFree(s->scratch);
-    s->scratch = nullptr;
+    wait_scene(s); // this scene's launches on any stream may still read it
+    scene_free(s, s->scratch);
     s->scratch_bytes = 0;
   }
-  hipError_t e = hipMalloc((void **)&s->scratch, bytes);
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
+  hipError_t e = scene_alloc(s, (void **)&s->scratch, bytes);
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync scratch: ") + hipGetErrorString(e));
   s->scratch_bytes = bytes;
   return RT_OK;
 }
@@ -695,20 +752,16 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
 // tiles became the tail, regrouped those tiles' sums: not bit-identical.)
 static int ensure_order(rt_scene *s, int n) {
   if (s->order_cap >= n) return RT_OK;
-  if (s->tile_cost) {
-    (void)hipDeviceSynchronize(); // a launch on any stream may still use them
-    (void)hipFree(s->tile_cost);
-    (void)hipFree(s->tile_order[0]);
-    (void)hipFree(s->tile_order[1]);
-  }
-  s->tile_cost = nullptr;
-  s->tile_order[0] = s->tile_order[1] = nullptr;
+  if (s->tile_cost) wait_scene(s); // this scene's launches on any stream may still use them
+  scene_free(s, s->tile_cost);
+  scene_free(s, s->tile_order[0]);
+  scene_free(s, s->tile_order[1]);
   s->order_cap = 0;
   s->order_ready = false;
-  hipError_t e = hipMalloc((void **)&s->tile_cost, (size_t)n * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMalloc((void **)&s->tile_order[0], (size_t)n * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc((void **)&s->tile_order[1], (size_t)n * sizeof(int32_t));
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc tile order: ") + hipGetErrorString(e));
+  hipError_t e = scene_alloc(s, (void **)&s->tile_cost, (size_t)n * sizeof(uint32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&s->tile_order[0], (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&s->tile_order[1], (size_t)n * sizeof(int32_t));
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync tile order: ") + hipGetErrorString(e));
   s->order_cap = n;
   return RT_OK;
 }
@@ -800,13 +853,12 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
 static int ensure_out(rt_scene *s, size_t bytes) {
   if (s->out_bytes >= bytes) return RT_OK;
   if (s->out_buf) {
-    (void)hipStreamSynchronize(s->stream);
-    (void)hipFree(s->out_buf);
-    s->out_buf = nullptr;
+    (void)hipStreamSynchronize(s->stream); // only the scene's own stream writes it
+    scene_free(s, s->out_buf);
     s->out_bytes = 0;
   }
-  hipError_t e = hipMalloc((void **)&s->out_buf, bytes);
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc output: ") + hipGetErrorString(e));
+  hipError_t e = scene_alloc(s, (void **)&s->out_buf, bytes);
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync output: ") + hipGetErrorString(e));
   s->out_bytes = bytes;
   return RT_OK;
 }
@@ -849,17 +901,24 @@ int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, 
   if ((rc = to_launch(f, &q, L))) return rc;
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)hip_stream; // NULL = the HIP null stream (HIP convention)
-  if (!auto_units) return launch(s, C, L, dev_rgb, nullptr, st);
+  if (!auto_units) {
+    rc = launch(s, C, L, dev_rgb, nullptr, st);
+    const int rn = note_stream(s, st); // what destroy / buffer growth wait for
+    return rc ? rc : rn;
+  }
   // the subset's own units: whole head tiles straight into dev_rgb, chunk
   // partials into the scratch, added in chunk order into dev_rgb (the
   // rt_multi shards' finish), all on `st`
   const SplitPlan sp = subset_plan(s, L);
   const int32_t *order = nullptr;
-  if ((rc = launch(s, C, L, dev_rgb, nullptr, st, &sp, &order))) return rc;
-  hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
-                                         order, dev_rgb, st);
-  if (e != hipSuccess) return hip_err(e, "tile chunk sum");
-  return RT_OK;
+  rc = launch(s, C, L, dev_rgb, nullptr, st, &sp, &order);
+  if (rc == RT_OK) {
+    hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
+                                           order, dev_rgb, st);
+    if (e != hipSuccess) rc = hip_err(e, "tile chunk sum");
+  }
+  const int rn = note_stream(s, st);
+  return rc ? rc : rn;
 }
 
 int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
@@ -1010,8 +1069,8 @@ int rt_multi_destroy(rt_multi *m) {
         DeviceGuard gs(s->device);
         (void)hipStreamSynchronize(s->stream);
       }
-    if (m->stage) (void)hipFree(m->stage);
-    if (m->frame) (void)hipFree(m->frame);
+    scene_free(m->scenes[0], m->stage); // stream-ordered on the root scene's stream
+    scene_free(m->scenes[0], m->frame);
   }
   for (rt_scene *s : m->scenes) rt_scene_destroy(s);
   delete m;
@@ -1156,13 +1215,11 @@ int rt_multi_render(rt_multi *m, const rt_frame *f, const rt_render_params *p, d
     DeviceGuard g(root->device);
     auto grow = [&](double *&buf, size_t &have, size_t bytes, const char *what) -> int {
       if (have >= bytes) return RT_OK;
-      if (buf) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(buf);
-        buf = nullptr;
-        have = 0;
-      }
-      hipError_t e = hipMalloc((void **)&buf, bytes);
+      // the last rt_multi_render synchronised every shard's stream and the
+      // root's before it returned: nothing still uses buf
+      scene_free(root, buf);
+      have = 0;
+      hipError_t e = scene_alloc(root, (void **)&buf, bytes);
       if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMalloc ") + what + ": " + hipGetErrorString(e));
       have = bytes;
       return RT_OK;
