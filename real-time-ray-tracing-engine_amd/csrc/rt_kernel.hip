@@ -42,72 +42,32 @@ namespace {
 using namespace rtp;
 // Idle lanes that trigger a refill while other lanes still trace (measured:
 // 16 for the plain instance, C3 +4 %; the rich instances lose with any delay).
-#ifndef RT_REGEN_MIN
-#ifndef RT_REGEN_FLAT
-#define RT_REGEN_FLAT 16
-#endif
-#ifndef RT_REGEN_PLAIN
-#define RT_REGEN_PLAIN 16
-#endif
-#define RT_REGEN_MIN(F) ((F) == F_FLAT ? RT_REGEN_FLAT : (((F) & ~F_BVH4) == 0 ? RT_REGEN_PLAIN : 1))
-#endif
-#ifndef RT_BLOCK_WAVES
-#define RT_BLOCK_WAVES 4
-#endif
-constexpr int kWaves = RT_BLOCK_WAVES; // waves (work units) per block
+#define RT_REGEN_MIN(F) ((F) == F_FLAT ? 16 : (((F) & ~F_BVH4) == 0 ? 16 : 1))
+constexpr int kWaves = 4; // waves (work units) per block
 // Flat instances (no BVH, nothing staged in LDS) run one-wave blocks: a
 // block's wave slots are released only when all of its waves have ended, so
 // with 4-wave blocks a slot idles until the slowest unit of its block is done
 // (measured: C2 +2.0 %, C4 +10.4 % over 4-wave blocks; 2-wave blocks +0.5 % /
 // +6.3 %; profiles/r03g_ab.log).  BVH instances keep 4-wave blocks: their
 // waves share the block's staged BVH prefix.
-#ifndef RT_FLAT_BLOCK_WAVES
-#define RT_FLAT_BLOCK_WAVES 1
-#endif
-constexpr int block_waves(unsigned f) { return (f & F_FLAT) ? RT_FLAT_BLOCK_WAVES : RT_BLOCK_WAVES; }
+constexpr int block_waves(unsigned f) { return (f & F_FLAT) ? 1 : kWaves; }
 // Waves per block of the persistent instance: one block per CU (16 = 4 SIMDs x
 // its 4-waves/SIMD target), so the CU's 160 KB of LDS holds ONE copy of the
 // staged BVH beside its 16 waves' stacks instead of four copies for four
 // 4-wave blocks (gfx950: a workgroup may own all 160 KB).
-#ifndef RT_PC_WAVES
-#define RT_PC_WAVES 16
-#endif
-constexpr int kPcWaves = RT_PC_WAVES;
+constexpr int kPcWaves = RT_PC_WAVES; // rt_layout.h
 // the persistent instance also stages the world items and spheres when they fit
-#ifndef RT_LDS_PRIMS
-#define RT_LDS_PRIMS 1
-#endif
 constexpr size_t kLdsPerCu = 160 * 1024;
 
 // Occupancy target per instance (waves per SIMD): the compiler may spill a few
 // registers to reach it.  Measured: 4 for the plain instance (C3
 // +12 % over 3), 3 for the rich ones (C4 +8.6 % over the 2 that 224 VGPRs give).
-#ifndef RT_WAVES_F0
-#define RT_WAVES_F0 4
-#endif
-#ifndef RT_WAVES_OTHER
-#define RT_WAVES_OTHER 3
-#endif
-#ifndef RT_WAVES_FLAT
-#define RT_WAVES_FLAT 4
-#endif
+#define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? 4 : (((F) & ~F_BVH4) == 0 ? 4 : 3))
 // Feature sets with a persistent chunked-frame instance (render_tiles<.., PC>,
 // whose waves pull work units from a counter): the plain BVH walks (C3 +3.4 %,
 // profiles/r02ab-af_*); the flat and the rich instances keep one unit per wave
 // -- the unit loop's extra live state cost them 2-20 %.
-#ifndef RT_KARG_FRESH
-#define RT_KARG_FRESH 1
-#endif
 #define RT_PERSIST_F(F) (((F) & ~F_BVH4) == 0)
-#define RT_WAVES_PER_EU(F) ((F) == F_FLAT ? RT_WAVES_FLAT : (((F) & ~F_BVH4) == 0 ? RT_WAVES_F0 : RT_WAVES_OTHER))
-// occupancy target of the persistent instances (default: their feature set's)
-#ifndef RT_WAVES_PC
-#ifdef RT_WAVES_PC_N
-#define RT_WAVES_PC(F) RT_WAVES_PC_N
-#else
-#define RT_WAVES_PC(F) RT_WAVES_PER_EU(F)
-#endif
-#endif
 
 // The launch fields read afresh from the kernarg segment at each work unit
 // (FRESH, the persistent instances): the asm hides the segment pointer's
@@ -181,12 +141,9 @@ __device__ __forceinline__ DLaunch launch_fields(const DLaunch &P) {
 // once per work unit, outside the path loop, so the one-unit instances need
 // not hold them in SGPRs across every path trip).  Scalar loads through the
 // asm-hidden segment pointer: they stay at the use, the scalar cache serves them.
-#ifndef RT_EPI_FRESH
-#define RT_EPI_FRESH 1 // non-flat instances only: the flat one measured -0.5 % kernel time with it (C2; C4 neutral); profiles/r03l_ab.log
-#endif
-#ifndef RT_EPI_FRESH_F
-#define RT_EPI_FRESH_F(F) (RT_EPI_FRESH != 0 && ((F) & F_FLAT) == 0)
-#endif
+// non-flat instances only: the flat one measured -0.5 % kernel time with it
+// (C2; C4 neutral); profiles/r03l_ab.log
+#define RT_EPI_FRESH_F(F) (((F) & F_FLAT) == 0)
 template <bool FRESH>
 __device__ __forceinline__ DCamera camera_fields(const DCamera &C) {
   if constexpr (FRESH) {
@@ -278,7 +235,7 @@ extern "C" hipError_t rtk_unit_times_clear(void) {
 // blocks of PCW waves (kPcWaves = one block per CU; kWaves when the traversal
 // stacks of 16 waves do not fit the CU's LDS, e.g. deep 4-wide trees)
 template <bool STATS, unsigned F, int PCW = 0>
-__global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(PCW ? RT_WAVES_PC(F) : RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
+__global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   constexpr bool PC = PCW > 0;
   constexpr int BW = PC ? PCW : block_waves(F); // waves per block
@@ -310,7 +267,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
   }
   if (S.n_lds_nodes > 0 || (PC && S.lds_items_pc > 0)) { // stage once per block
-    if constexpr ((F & F_BVH4) != 0 || !RT_LDS_TRIPLE) {
+    if constexpr ((F & F_BVH4) != 0) {
       const int4 *src = reinterpret_cast<const int4 *>(S.nodes);
       int4 *dst = reinterpret_cast<int4 *>(lnodes_g);
       const int n16 = max(0, S.n_lds_nodes) * (kNodeBytes / 16);
@@ -323,7 +280,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       const uint2 *src = reinterpret_cast<const uint2 *>(S.nodes);
       uint2 *dst = reinterpret_cast<uint2 *>(lnodes_g);
       const int n8 = max(0, S.n_lds_nodes) * 10;
-      const bool whole = RT_SLAB_FMA && RT_SLAB_SIGN && S.n_lds_nodes >= S.n_nodes; // trace()'s LDS-only walk
+      const bool whole = S.n_lds_nodes >= S.n_nodes; // trace()'s LDS-only walk
       for (int k = threadIdx.x; k < n8; k += blockDim.x) {
         const int i = k / 10, j = k - 10 * (k / 10);
         const int a = j / 3, m = j - 3 * (j / 3);
@@ -347,7 +304,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
     __syncthreads();
   }
-#if RT_LDS_PERLIN
   if constexpr ((F & F_NOISE) != 0) { // the Perlin table (tex_value), once per block
     if (S.lds_perlin) {
       const int4 *src = reinterpret_cast<const int4 *>(S.perlin);
@@ -356,7 +312,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       __syncthreads();
     }
   }
-#endif
   // work unit = (local tile, stratum chunk).  Persistent launches (P.unit_ctr
   // set, grid = the resident waves): a wave's first unit is its static slot,
   // the next ones come from the agent-scope counter (initialised by the host to
@@ -383,7 +338,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
 #if RT_UNIT_TIMES
   const unsigned long long t_unit0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  const DLaunch PU = launch_fields<PC && RT_KARG_FRESH>(P);
+  const DLaunch PU = launch_fields<PC>(P);
   // (wave-uniform) head unit: tile unit / head_chunks; tail unit: a chunk of
   // the tail tile n_head + (unit - head units) / n_chunks
   const int head_units = PU.n_head * PU.head_chunks;
@@ -456,7 +411,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     if (ps.active) {
       if (STATS) n_segments++;
       const uint32_t nv0 = cnt.nodes;
-      bool cont = segment<STATS, F, PC && RT_LDS_PRIMS>(
+      bool cont = segment<STATS, F, PC>(
           S, C, ps, key, stk, lnodes, cnt, (RT_LDS LeafPool *)&leaf_pool[RT_LEAF_SHARE_F(F) ? wv : 0], lp);
       if (STATS) v_trace = cnt.nodes - nv0;
       if (!cont) {
@@ -487,11 +442,11 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   // ---- tile epilogue: one coalesced store per pixel
   {
     // the epilogue's launch fields, camera width / scale and output pointer
-    // read afresh (RT_EPI_FRESH): once per unit, outside the path loop, so the
+    // read afresh (RT_EPI_FRESH_F): once per unit, outside the path loop, so the
     // one-unit instances need not hold them in SGPRs across every path trip
     constexpr bool kEpiFresh = RT_EPI_FRESH_F(F);
     const DCamera Ce = camera_fields<kEpiFresh>(C);
-    const DLaunch PE = launch_fields<(PC && RT_KARG_FRESH) || kEpiFresh>(P);
+    const DLaunch PE = launch_fields<PC || kEpiFresh>(P);
     int i = x0 + (lane & 7), j = y0 + (lane >> 3);
     // whole units: the frame (pixels outside the image are not written) or
     // the compact tile layout; split units: their chunk's partial sums
@@ -505,7 +460,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
         sy = Ce.scale * sy;
         sz = Ce.scale * sz;
       }
-      double *const ob = out_arg<(PC && RT_KARG_FRESH) || kEpiFresh>(out);
+      double *const ob = out_arg<PC || kEpiFresh>(out);
       const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
       double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
                   : PE.compact ? ob + 3 * ((size_t)(RT_ORDER_F(F) ? order_tile(PE, unit) : unit) * 64 + lane)
@@ -804,8 +759,8 @@ extern "C" hipError_t rtk_lds_plan_pc(int features, int stack_depth, int force_w
   }
   return hipSuccess;
 }
-extern "C" int rtk_lds_prims_enabled(void) { return RT_LDS_PRIMS; }
-extern "C" int rtk_lds_perlin_enabled(void) { return RT_LDS_PERLIN; }
+extern "C" int rtk_lds_prims_enabled(void) { return 1; }
+extern "C" int rtk_lds_perlin_enabled(void) { return 1; }
 
 // Lets a persistent instance's blocks use more than 64 KB of dynamic LDS: set
 // once per device and function, to the most any scene's plan can ask for (the

@@ -29,13 +29,9 @@
 #define RT_N_STATS 24      // counters of the STATS kernel instance (rt_path_stats)
 #define RT_STACK_DEPTH 32 // traversal stack entries per lane (BVH depth is capped below it)
 #define RT_STACK_DEPTH4 64 // 4-wide walks push up to three entries per level
-#ifndef RT_PC_WAVES
 #define RT_PC_WAVES 16    // waves per block of the persistent instance (one block per CU)
-#endif
 #define RT_PC_BLOCK_WAVES RT_PC_WAVES
-#ifndef RT_FLAT_MAX
 #define RT_FLAT_MAX 8 // worlds of at most this many items are one flat leaf (no BVH walk)
-#endif
 
 enum DItemKind {
   I_SPHERE = 0,
@@ -113,11 +109,8 @@ static_assert(sizeof(DNode) == 64, "DNode layout");
 // lo planes, hi planes and lo planes again, so that a ray's near and far plane
 // pairs (sign-picked: near = lo for 1/d_a >= 0, hi otherwise) are adjacent for
 // either sign -- one 16-B read per axis at byte 24 a + 8 s_a instead of two
-// 8-B reads at unrelated offsets (rt_path.h load_planes_l).  RT_LDS_TRIPLE 0:
-// nodes are staged as DNode (A/B).
-#ifndef RT_LDS_TRIPLE
-#define RT_LDS_TRIPLE 1
-#endif
+// 8-B reads at unrelated offsets (rt_path.h load_planes_l).  (Staged as
+// DNode instead: C3 -1.7 %, profiles/r04l_c3_ab.log.)
 struct DNodeL {
   float p[3][3][2]; // p[axis][0] = lo[axis][*], p[axis][1] = hi[axis][*], p[axis][2] = lo[axis][*]
   int32_t entry[2];
@@ -227,7 +220,7 @@ struct DScene {      // kernel argument (by value)
 #define RT_FEAT_BVH4 32  // the world BVH is 4-wide (DNode4); never with RT_FEAT_FLAT
 // bytes per BVH node staged in LDS (DNode4 / DNodeL / DNode)
 #define RT_LDS_NODE_BYTES(features)                                                                \
-  (((features) & RT_FEAT_BVH4) ? (int)sizeof(DNode4) : RT_LDS_TRIPLE ? (int)sizeof(DNodeL) : (int)sizeof(DNode))
+  (((features) & RT_FEAT_BVH4) ? (int)sizeof(DNode4) : (int)sizeof(DNodeL))
 
 // LDS plan of one render instance (rtk_lds_plan): its occupancy target and
 // what the per-block LDS share at that occupancy leaves for staged BVH nodes.

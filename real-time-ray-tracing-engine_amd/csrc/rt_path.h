@@ -30,9 +30,6 @@
 
 namespace rtp {
 
-#ifndef RT_PHILOX_ROUNDS
-#define RT_PHILOX_ROUNDS 10 // Philox4x32-10 (Random123 default); other values: timing experiments only
-#endif
 constexpr double kInf = __builtin_huge_val();
 constexpr double kPi = 3.1415926535897932385;
 constexpr uint32_t kCamTag = 0xFFFFFFFFu;
@@ -60,11 +57,8 @@ RT_HD RT_FI V3 cross(V3 a, V3 b) {
 // instructions.  Used where the input is a unit-range quantity known to be 0 or
 // far above 2^-767 (u = k 2^-32, 1 - u, 1 - x^2 of a double |x| <= 1, a squared
 // length compared against 1e-16); the root of a discriminant keeps sqrt().
-#ifndef RT_SQRT_N
-#define RT_SQRT_N 1
-#endif
 RT_HD RT_FI double sqrt_n(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SQRT_N
+#if defined(__HIP_DEVICE_COMPILE__)
   double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = 0.5 * y;
   const double r = fma(-h, g, 0.5);
@@ -83,11 +77,8 @@ RT_HD RT_FI double sqrt_n(double x) {
 // division lowering with numerator 1 (v_rcp_f64, two Newton steps, one
 // Markstein correction) without v_div_scale (a no-op in that range) and with a
 // +inf class select in place of v_div_fixup — 7 of 11 instructions.
-#ifndef RT_RCP_N
-#define RT_RCP_N 1
-#endif
 RT_HD RT_FI double rcp_n(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_RCP_N
+#if defined(__HIP_DEVICE_COMPILE__)
   const double y0 = __builtin_amdgcn_rcp(x);
   double e = fma(-x, y0, 1.0);
   const double y1 = fma(y0, e, y0);
@@ -175,7 +166,7 @@ RT_HD RT_FI void philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
   if constexpr (KB) asm volatile("" : "+s"(k0), "+s"(k1));
 #endif
 #pragma unroll
-  for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
+  for (int r = 0; r < 10; ++r) { // Philox4x32-10 (Random123 default)
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -211,10 +202,7 @@ RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]
 // fdlibm/FreeBSD k_sin/k_cos minimax polynomials.  Max |error| 1.4e-16 against
 // the exact sin(2 pi u) (the reference's sin(fl(2 pi u)) is itself up to 4.4e-16
 // from it); tested in tests/test_emulator.py.
-#ifndef RT_SINCOS_2PI
-#define RT_SINCOS_2PI 1
-#endif
-// Polynomial constants at their use (RT_KCONST, device): fma(a, b, K) as ONE
+// Polynomial constants at their use (device, RT_KCONST_MODE 1): fma(a, b, K) as ONE
 // v_fma_f64 whose addend K is put into an SGPR pair by two s_mov_b32 right
 // there (volatile, so not hoisted).  Written as plain fma, the compiler hoists
 // each fp64 coefficient out of the path loop into a VGPR pair (sincos: 10
@@ -222,10 +210,7 @@ RT_HD RT_FI void u01x4(const Key &k, uint32_t bounce, uint32_t slot, double u[4]
 // it selects the tied v_fmac_f64 form, copies the constant into the
 // accumulator before every step (v_mov_b64 + v_fmac_f64).  Same correctly
 // rounded fma, same bits.
-#ifndef RT_KCONST
-#define RT_KCONST 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
+#if defined(__HIP_DEVICE_COMPILE__)
 template <uint64_t K>
 __device__ __forceinline__ double kconst_s() { // K's double in an SGPR pair, materialised here
   uint32_t lo, hi;
@@ -253,22 +238,17 @@ __device__ __forceinline__ double fma_kk(double a) { // fma(a, B, K): B from SGP
 // VGPR spills 20 -> 4), the flat instance C2 -1 %, the rich C4 -8 % (its SGPRs
 // are already spilled into VGPR lanes; constants put into VGPRs by v_mov at
 // their use instead: C4 -7.6 %, r03x_ab.log): used by the plain BVH instances only.
-#ifndef RT_KCONST_F
-#define RT_KCONST_F(F) (RT_KCONST != 0 && ((F) & ~F_BVH4) == 0)
-#endif
+#define RT_KCONST_F(F) (((F) & ~F_BVH4) == 0)
 // KC: 1 = the polynomial constants at their use in SGPRs (above), 0 = plain fma
-#ifndef RT_KCONST_MODE
 #define RT_KCONST_MODE(F) (RT_KCONST_F(F) ? 1 : 0)
-#endif
 template <int KC = 0>
 RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
-#if RT_SINCOS_2PI
   const double t = 4.0 * u;
   const double q = floor(t + 0.5);
   const double x = (t - q) * 1.5707963267948966;
   const double z = x * x;
   double ps, sn, pc;
-#if defined(__HIP_DEVICE_COMPILE__) && RT_KCONST
+#if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (KC == 1) {
     ps = FMA_K(z, FMA_K(z, FMA_K(z, FMA_KK(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
                                  2.75573137070700676789e-06), -1.98412698298579493134e-04),
@@ -295,9 +275,6 @@ RT_HD RT_FI void sincos_2pi(double u, double &s, double &c) {
   c = (qi & 1) ? sn : cn;
   if (qi >= 2) s = -s;
   if (qi == 1 || qi == 2) c = -c;
-#else
-  sincos(2.0 * kPi * u, &s, &c);
-#endif
 }
 
 // ---------------------------------------------------------------- features
@@ -322,9 +299,6 @@ enum : unsigned {
 // (TwoSum, exact product tail by FMA), then the fdlibm kernels (k_sin.c /
 // k_cos.c, Sun Microsystems 1993, freely redistributable) on |r| <= pi/4.
 // Larger or non-finite arguments go to the library sin out of line.
-#ifndef RT_SIN_N
-#define RT_SIN_N 1 // 0: the library sin (A/B builds)
-#endif
 RT_HD __attribute__((noinline)) double sin_wide(double x) { return sin(x); }
 RT_HD RT_FI double sin_n(double x) {
   if (!(fabs(x) < 0x1p20)) return sin_wide(x);
@@ -364,16 +338,13 @@ RT_HD RT_FI double sin_n(double x) {
 // u-1: the same doubles for every input (0*x + y == y, x - 0 == x here; NaN stays
 // NaN), without the dead multiplies.  Corner order and the ((fi*fj)*fk)*dot
 // grouping are the reference's.
-// RT_PERLIN_LERP (the device build): the same trilinear Hermite blend as
+// The device build: the same trilinear Hermite blend as
 // repeated linear interpolation -- 8 corner dot products as FMAs, then 4 + 2 +
 // 1 lerps a + t (b - a) -- instead of 8 products of three weights: about 40
 // instead of 70 fp64 operations per octave.  The grouping and the FMAs change
 // the rounding of the noise value (relative differences ~1e-16; nothing
 // branches on it, it only scales the albedo), so the host build (emulator)
 // keeps the reference's order and images agree with the oracle to ~1e-15.
-#ifndef RT_PERLIN_LERP
-#define RT_PERLIN_LERP 1 // C4 +6.6 % (4-wave blocks, r03g) and +5.3 % (one-wave blocks: r03h 3,207 vs r03j 3,047)
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 // The device form's blend of one octave from its cell offsets (u, v, w), their
 // Hermite weights and the six permutation entries of the cell's corners.
@@ -402,7 +373,7 @@ RT_HD double perlin_noise(PP P, V3 p) {
   double u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int xi = (int)fx, yi = (int)fy, zi = (int)fz;
   double uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
-#if defined(__HIP_DEVICE_COMPILE__) && RT_PERLIN_LERP
+#if defined(__HIP_DEVICE_COMPILE__)
   const int px0 = P->px[xi & 255], px1 = P->px[(xi + 1) & 255];
   const int py0 = P->py[yi & 255], py1 = P->py[(yi + 1) & 255];
   const int pz0 = P->pz[zi & 255], pz1 = P->pz[(zi + 1) & 255];
@@ -425,9 +396,6 @@ RT_HD double perlin_noise(PP P, V3 p) {
   return acc;
 }
 
-#ifndef RT_LDS_PERLIN
-#define RT_LDS_PERLIN 1
-#endif
 using PerlinLds = DPerlin;
 #if defined(__HIP__)
 // The block's LDS copy of the scene's Perlin table (9 KB; allocated in the noise instances only -- the ones that call this).
@@ -443,9 +411,6 @@ __device__ __forceinline__ const RT_LDS PerlinLds *perlin_lds() {
 // octave blends) it measured C4 -1.5 % with 7 more spilled VGPRs
 // (profiles/r03s_ab.log).  fp32 octaves on an fp32 gradient copy: C4 +0.25 %,
 // within noise (r03r_ab.log), so the reference's fp64 arithmetic is kept.
-#ifndef RT_TURB_NOUNROLL
-#define RT_TURB_NOUNROLL 1
-#endif
 
 template <unsigned F>
 RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
@@ -463,9 +428,7 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
       auto turb = [&](auto P) { // PerlinNoise::turb(p, 7)
         double acc = 0.0, wgt = 1.0;
         V3 q = p;
-#if RT_TURB_NOUNROLL
 #pragma unroll 1
-#endif
         for (int i = 0; i < 7; i++) {
           acc += wgt * perlin_noise(P, q);
           wgt *= 0.5;
@@ -473,7 +436,7 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
         }
         return acc;
       };
-#if defined(__HIP_DEVICE_COMPILE__) && RT_LDS_PERLIN
+#if defined(__HIP_DEVICE_COMPILE__)
       // the scene's one Perlin table staged in LDS by the block (S.lds_perlin):
       // 7 octaves x (6 permutation + 8 gradient reads), two dependent rounds
       // each, at LDS rather than L1/L2 latency
@@ -481,11 +444,7 @@ RT_HD V3 tex_value(const DScene &S, int t, V3 p) {
 #else
       const double acc = turb(&S.perlin[T.perlin]);
 #endif
-#if RT_SIN_N
       double f = 1 + sin_n(T.scale * p.z + 10 * fabs(acc));
-#else
-      double f = 1 + sin(T.scale * p.z + 10 * fabs(acc));
-#endif
       return f * v3(0.5, 0.5, 0.5);
     }
     break;
@@ -517,12 +476,6 @@ RT_HD RT_FI V3 sphere_center(const DSphere &s, double tm, bool moving) {
 // per-call operand check with a division fallback was measured and costs more
 // than the saving (C2 -3 %).  Checked on the host over 4e8 random operand pairs
 // (incl. all-ones significands): 0 differences.
-#ifndef RT_MK_SPHERE
-#define RT_MK_SPHERE 1
-#endif
-#ifndef RT_MK_PI
-#define RT_MK_PI 1
-#endif
 RT_HD RT_FI double div_mk(double x, double b, double y) {
   const double q = x * y;
   const double r = fma(-q, b, x);
@@ -541,9 +494,9 @@ RT_HD RT_FI bool sphere_root(const DSphere &s, const Ray &r, double a, double tm
   if (disc < 0) return false;
   double sq = sqrt(disc);
   // mk: ya = RN(1/a) shared by every root of one ray (div_mk), else the division
-  double t = (RT_MK_SPHERE && mk) ? div_mk(h - sq, a, ya) : (h - sq) / a;
+  double t = mk ? div_mk(h - sq, a, ya) : (h - sq) / a;
   if (!(tmin < t && t < tmax)) {
-    t = (RT_MK_SPHERE && mk) ? div_mk(h + sq, a, ya) : (h + sq) / a;
+    t = mk ? div_mk(h + sq, a, ya) : (h + sq) / a;
     if (!(tmin < t && t < tmax)) return false;
   }
   root = t;
@@ -576,17 +529,9 @@ RT_HD RT_FI void sphere_record(const DSphere &s, const Ray &r, double t, int mat
 //    (t would be 0) and otherwise accepts only with d_k, o_k (finite t) and
 //    o_i, d_i, o_j, d_j (finite alpha, beta) finite -- every component.
 // The quad's own values are finite (checked when aa is set).
-#ifndef RT_QUAD_AA
-#define RT_QUAD_AA 1
-#endif
-#ifndef RT_UNIFORM_LOADS
-#define RT_UNIFORM_LOADS 1 // scalar loads of wave-uniform scene records (ldu)
-#endif
 // ... in the plain flat instance (C2 +2.7 %); the rich flat instances have no
 // SGPRs to spare for the records (C4 -1.6 %; profiles/r03d_ab.log)
-#ifndef RT_UNIFORM_LOADS_F
-#define RT_UNIFORM_LOADS_F(F) (RT_UNIFORM_LOADS != 0 && (F) == F_FLAT)
-#endif
+#define RT_UNIFORM_LOADS_F(F) ((F) == F_FLAT)
 RT_HD RT_FI double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); } // no private array
 // SEL: the quad's axis components picked by value selects, not by an indexed
 // load -- for a record held in registers (a uniform scalar load, ldu), where
@@ -638,9 +583,6 @@ RT_HD RT_FI bool quad_t_aa_c(const DQuad &q, const Ray &r, double tmin, double t
 // Dispatch on a WAVE-UNIFORM aa (the flat list walk, the light loops: one
 // record for every lane): scalar branches to the constant-axis form.  A
 // per-lane aa (BVH leaves) keeps quad_t_aa: a switch would serialise there.
-#ifndef RT_QUAD_AXES
-#define RT_QUAD_AXES 1
-#endif
 RT_HD RT_FI bool quad_t_aa_u(const DQuad &q, const Ray &r, double tmin, double tmax, double &t) {
   switch (q.aa & 63) {
   case 0 | 1 << 2 | 2 << 4: return quad_t_aa_c<0, 1, 2>(q, r, tmin, tmax, t);
@@ -654,10 +596,10 @@ RT_HD RT_FI bool quad_t_aa_u(const DQuad &q, const Ray &r, double tmin, double t
 template <bool SEL = false, bool UAX = false> // UAX: q is the same record in every lane
 RT_HD RT_FI bool quad_t(const DQuad &q, const Ray &r, double tmin, double tmax,
                                        double &t) { // Plane.cpp:76-100
-  if constexpr (UAX && RT_QUAD_AXES) {
-    if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa_u(q, r, tmin, tmax, t);
+  if constexpr (UAX) {
+    if (q.aa >= 0) return quad_t_aa_u(q, r, tmin, tmax, t);
   }
-  if (RT_QUAD_AA && q.aa >= 0) return quad_t_aa<SEL>(q, r, tmin, tmax, t);
+  if (q.aa >= 0) return quad_t_aa<SEL>(q, r, tmin, tmax, t);
   V3 n = ld3(q.n);
   double denom = dot(n, r.d);
   if (fabs(denom) < 1e-8) return false;
@@ -794,7 +736,7 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
     } else { // quad_t without its interval test
       const DQuad &q = S.quads[it.idx];
       double tt;
-      if (RT_QUAD_AA && q.aa >= 0) {
+      if (q.aa >= 0) {
         if (!quad_t_aa(q, lr, -kInf, kInf, tt)) continue;
       } else {
         V3 n = ld3(q.n);
@@ -880,9 +822,6 @@ RT_HD RT_FI bool boundary_span(const DScene &S, const DMedium &M, const Ray &r, 
 // Proven on the host against the reference's own ConstantMedium boundary
 // queries (tests/test_medium_box.py: edge, corner, grazing and axis-parallel
 // rays, oracle/_ref) and on the device against boundary_span bit for bit.
-#ifndef RT_BOX_SPAN
-#define RT_BOX_SPAN 1
-#endif
 RT_HD RT_FI int box_span(const DScene &S, const DMedium &M, const Ray &mr, double &t1,
                          double &t2) {
   const Ray r = M.bxf_count ? to_local(S, M.bxf_first, M.bxf_count, mr) : mr;
@@ -938,7 +877,7 @@ RT_HD bool medium_t(const DScene &S, const DItem &it, const Ray &wr, double tmin
   const DMedium M = S.media[it.idx];
   Ray r = it.xf_count ? to_local(S, it.xf_first, it.xf_count, wr) : wr;
   double t1, t2;
-  const int rc = (RT_BOX_SPAN && M.box) ? box_span(S, M, r, t1, t2) : -2;
+  const int rc = M.box ? box_span(S, M, r, t1, t2) : -2;
   box_path = rc == -2 ? -1 : rc >= 0;
   if (rc == 0) return false;
   if (rc < 0 && !boundary_span(S, M, r, t1, t2)) return false;
@@ -1005,9 +944,6 @@ RT_HD RT_FI float f32_dn(double x) { // largest float <= x (x not NaN)
 // 1/d for the slab test in fp32: v_rcp_f32 (1 ulp) of the rounded direction,
 // instead of an fp64 division rounded to fp32 (relative error <= 2^-22.4 vs
 // 2^-24; the far-distance growth below still covers the slab error with room).
-#ifndef RT_RCP32
-#define RT_RCP32 1
-#endif
 RT_HD RT_FI float rcp32(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_rcpf(x);
@@ -1015,14 +951,10 @@ RT_HD RT_FI float rcp32(float x) {
   return 1.0f / x;
 #endif
 }
-#if RT_RCP32
 constexpr float kSlabGrow = 1.0f + 0x1p-19f;
-#else
-constexpr float kSlabGrow = 1.0f + 0x1p-20f;
-#endif
 constexpr float kInvClamp = 1e30f; // finite 1/d: a 0 * inf NaN would drop a box
 
-// Slab form.  RT_SLAB_FMA=1: t = fma(plane, 1/d, -P) with P = RN32(o/d) per ray
+// Slab form (FMA): t = fma(plane, 1/d, -P) with P = RN32(o/d) per ray
 // and axis — one fp32 FMA per plane instead of a subtract and a multiply.  P's
 // rounding is an ABSOLUTE error eps <= |P| 2^-23 in every plane distance (the
 // subtract form's errors are all relative), so the test adds an absolute slack
@@ -1037,9 +969,6 @@ constexpr float kInvClamp = 1e30f; // finite 1/d: a 0 * inf NaN would drop a box
 // FMA: the BVH instances (one ray feeds many box tests); the flat instances
 // single medium-box cull keeps the subtract form, whose per-ray setup is
 // cheaper (measured: C3 +2.8 %, C4 -6.5 % with FMA everywhere).
-#ifndef RT_SLAB_FMA
-#define RT_SLAB_FMA 1
-#endif
 template <bool FMA> struct RayF;
 template <> struct RayF<false> { // per-ray fp32 slab-test constants, subtract form
   float oa[3], ob[3], inv[3];
@@ -1054,11 +983,7 @@ RT_HD RT_FI RayF<FMA> ray_f32(const Ray &r) {
   float pm = 0.0f;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-#if RT_RCP32
     float iv = rcp32((float)d[a]);
-#else
-    float iv = (float)(1.0 / d[a]);
-#endif
     q.inv[a] = fminf(fmaxf(iv, -kInvClamp), kInvClamp);
     if constexpr (FMA) {
       const double pd = fmin(fmax((double)q.inv[a] * o[a], -1e37), 1e37); // NaN o: NaN
@@ -1125,7 +1050,7 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
   h0 = slab_hit(q, lo0, hi0, tmin32, cl32, t0);
   h1 = slab_hit(q, lo1, hi1, tmin32, cl32, t1);
 }
-// Node planes picked by the ray's direction signs (RT_SLAB_SIGN) -- the
+// Node planes picked by the ray's direction signs -- the
 // binary walk over a fully staged tree (C3: +8 %, C5: +8 %, profiles/
 // r04b_slab_sign_ab.log) and every 4-wide visit (100k / 1M spheres +10 %,
 // r04c_arity_sign_ab.log): for an axis with 1/d >= 0 the lo plane
@@ -1137,9 +1062,6 @@ RT_HD RT_FI void slab_hit2(const RayF<true> &q, const DNode &N, float tmin32, fl
 // `po` into the node (lo[a][*] at 8a, hi[a][*] at 24 + 8a): six 8-B LDS reads
 // instead of the twelve planes, and no min / max per plane pair -- the visit
 // drops from 36 to 24 slab VALU plus the six read addresses.
-#ifndef RT_SLAB_SIGN
-#define RT_SLAB_SIGN 1
-#endif
 struct PlaneOff { // per-ray byte offsets of the near planes of each axis in a DNode / DNode4
   int n[3];
 };
@@ -1152,7 +1074,7 @@ RT_HD RT_FI PlaneOff plane_offsets(const RayF<true> &q) {
   for (int a = 0; a < 3; ++a) o.n[a] = 4 * W * a + (q.inv[a] < 0.0f ? 12 * W : 0);
   return o;
 }
-// in a DNodeL (binary nodes staged in LDS, RT_LDS_TRIPLE): the near pair at
+// in a DNodeL (binary nodes staged in LDS, rt_layout.h): the near pair at
 // 24 a + 8 s_a, the far pair 8 B after it
 RT_HD RT_FI PlaneOff plane_offsets_l(const RayF<true> &q) {
   PlaneOff o;
@@ -1413,7 +1335,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
   bool best_full = false;
   if constexpr ((F & F_MEDIA) != 0) {
     const uint64_t t0 = STATS ? clk() : 0;
-    constexpr bool kFma = RT_SLAB_FMA && !kFlat;
+    constexpr bool kFma = !kFlat;
     const RayF<kFma> q = ray_f32<kFma>(r);
     const float tmin32 = f32_dn(tmin);
     float cl32 = f32_up(closest);
@@ -1465,7 +1387,7 @@ RT_HD RT_FI bool trace_tail(const DScene &S, const Ray &r, Hit &h, const Key &ke
 // Closest hit over the world BVH.  Primitive items record only (t, item) during
 // traversal and build the hit record once at the end; media build theirs when hit.
 // `lnodes` is the LDS copy of nodes [0, S.n_lds_nodes): DNode4 for 4-wide trees,
-// DNodeL for binary ones (RT_LDS_TRIPLE; the host emulator passes the same forms
+// DNodeL for binary ones (the host emulator passes the same forms
 // of the whole tree).
 template <bool STATS, unsigned F, bool LP = false>
 RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
@@ -1476,14 +1398,14 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
   double closest = kInf;
   int best = -1;
   const double a = len2(r.d);
-  const double ya = RT_MK_SPHERE ? 1.0 / a : 0.0; // one reciprocal per ray for every sphere root
+  const double ya = 1.0 / a; // one reciprocal per ray for every sphere root
   // F_FLAT instances (small worlds, SAH root is one leaf) have no BVH walk; they
   // need the fp32 slab constants only for the medium box cull, and they skip
   // the center.at(time) arithmetic when no sphere moves (a wave-uniform flag).
   constexpr bool kFlat = (F & F_FLAT) != 0;
   constexpr bool kBoxes = !kFlat || (F & F_MEDIA) != 0;
   const bool moving = kFlat ? !S.static_spheres : true;
-  constexpr bool kFma = RT_SLAB_FMA && !kFlat;
+  constexpr bool kFma = !kFlat;
   RayF<kFma> q{};
   float tmin32 = 0.0f;
   float cl32 = __builtin_huge_valf(); // f32_up(closest)
@@ -1655,8 +1577,8 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
       return *top;
     };
     [[maybe_unused]] PlaneOff po{};
-    if constexpr (kFma && RT_SLAB_SIGN)
-      po = ((F & F_BVH4) == 0 && RT_LDS_TRIPLE) ? plane_offsets_l(q) : plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
+    if constexpr (kFma)
+      po = (F & F_BVH4) == 0 ? plane_offsets_l(q) : plane_offsets<(F & F_BVH4) ? 4 : 2>(q);
     int cur;
     int lf = 0, ln = 0;
     if (S.root_is_leaf) {
@@ -1678,7 +1600,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
           if (STATS) cnt.nodes++;
           float tn[4];
           int en[4];
-          if constexpr (kFma && RT_SLAB_SIGN) {
+          if constexpr (kFma) {
             NodePlanes<4> pl;
             if (cur < S.n_lds_nodes)
               load_planes<4>(pl, (const RT_LDS char *)lnodes4, cur * (int)sizeof(DNode4), po);
@@ -1753,24 +1675,20 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             float tn0, tn1;
             bool h0, h1;
             int e0, e1;
-            if constexpr (kFma && RT_SLAB_SIGN && LDS_ONLY) {
+            if constexpr (kFma && LDS_ONLY) {
               // the whole tree staged: sign-picked planes from LDS.  (From the
               // node table in memory the six 8-B loads instead of four 16-B
               // ones lost 14-17 % on 100k-1M spheres, and a per-lane choice
               // between the two forms runs both slab passes in a mixed wave:
               // -6.5 %, profiles/r04b_arity_sign_ab.log, r04c_arity_sign_ab.log.)
               NodePlanes<2> pl;
-              if constexpr (RT_LDS_TRIPLE) // cur: the node's byte offset (entries staged so)
-                load_planes_l(pl, (const RT_LDS char *)lnodes, cur, po);
-              else
-                load_planes<2>(pl, (const RT_LDS char *)lnodes, cur * (int)sizeof(DNode), po);
+              load_planes_l(pl, (const RT_LDS char *)lnodes, cur, po); // cur: the node's byte offset (entries staged so)
               slab2_planes(q, pl, tmin32, cl32, tn0, tn1, h0, h1);
               e0 = pl.en[0];
               e1 = pl.en[1];
             } else {
               DNode N;
               if (cur < S.n_lds_nodes) {
-#if RT_LDS_TRIPLE
                 const RT_LDS DNodeL &L = ((const RT_LDS DNodeL *)lnodes)[cur];
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
@@ -1779,30 +1697,12 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
                     N.lo[a][k] = L.p[a][0][k];
                     N.hi[a][k] = L.p[a][1][k];
                   }
-#else
-                const RT_LDS DNode &L = lnodes[cur];
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                  for (int k = 0; k < 2; ++k) {
-                    N.lo[a][k] = L.lo[a][k];
-                    N.hi[a][k] = L.hi[a][k];
-                  }
-#endif
                 N.entry[0] = L.entry[0];
                 N.entry[1] = L.entry[1];
               } else {
                 N = S.nodes[cur];
               }
-#if RT_SLAB_FMA
               slab_hit2(q, N, tmin32, cl32, tn0, tn1, h0, h1);
-#else
-              const float lo0[3] = {N.lo[0][0], N.lo[1][0], N.lo[2][0]}, hi0[3] = {N.hi[0][0], N.hi[1][0], N.hi[2][0]};
-              const float lo1[3] = {N.lo[0][1], N.lo[1][1], N.lo[2][1]}, hi1[3] = {N.hi[0][1], N.hi[1][1], N.hi[2][1]};
-              tn0 = slab(q, lo0, hi0, tmin32, cl32);
-              tn1 = slab(q, lo1, hi1, tmin32, cl32);
-              h0 = tn0 != __builtin_huge_valf(), h1 = tn1 != __builtin_huge_valf();
-#endif
               e0 = N.entry[0];
               e1 = N.entry[1];
             }
@@ -1822,7 +1722,7 @@ RT_HD RT_FI bool trace(const DScene &S, const Ray &r, Hit &h, const Key &key,
             }
           }
         };
-        if (kFma && RT_SLAB_SIGN && S.n_lds_nodes >= S.n_nodes)
+        if (kFma && S.n_lds_nodes >= S.n_nodes)
           walk(UTag<true>{});
         else
           walk(UTag<false>{});
@@ -1912,7 +1812,7 @@ RT_HD double lights_pdf(const DScene &S, V3 org, V3 dir, Counters &cnt) {
 }
 
 // SC: sincos(2 pi r1) arrives precomputed in (sp1, cp1) -- the caller's one
-// sincos shared with the other shading branches (shade, RT_SHADE_SINCOS)
+// sincos shared with the other shading branches (shade, kSc)
 template <int KC = 0, bool SC = false>
 RT_HD V3 lights_random(const DScene &S, V3 org, double upick, double r1, double r2,
                        double sp1 = 0.0, double cp1 = 0.0) {
@@ -1980,18 +1880,10 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 // L = e + a*L' sums emission only where a path ends (lights never scatter), so the
 // forward form needs no radiance register: the terminal T x value is the sample.
 // The material half of a segment, after the closest hit `h` of ps.ray.
-#ifndef RT_SHADE_MERGE
-#define RT_SHADE_MERGE 1
-#endif
 // Measured (profiles/r02w_shade_merge_ab.log): C3 (plain BVH instance, mixed
 // Lambertian / metal / glass) +2 %; C2 (flat, Lambertian only: the selects are
 // pure overhead) -2 %, C4 -1 % (more spills): merged in the plain BVH instances only.
-#ifndef RT_SHADE_MERGE_F
-#define RT_SHADE_MERGE_F(F) (RT_SHADE_MERGE != 0 && ((F) & ~F_BVH4) == 0)
-#endif
-#ifndef RT_SHADE_SINCOS
-#define RT_SHADE_SINCOS 1
-#endif
+#define RT_SHADE_MERGE_F(F) (((F) & ~F_BVH4) == 0)
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
                        const Hit &h, Counters &cnt) {
@@ -2127,9 +2019,9 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   // azimuth, a = d0), the cosine direction (a = d0) and the isotropic
   // direction (a = d1) a lane takes: the wave runs it once instead of once
   // per branch that any lane takes -- the same operation on the same operand
-  // for every lane (RT_SHADE_SINCOS; the merged-shading instances have theirs).
+  // for every lane (the merged-shading instances have theirs).
   // C4 +2.4 %, frames bit-identical (profiles/r05h_*).
-  constexpr bool kSc = RT_SHADE_SINCOS && !kMerge && (F & F_LIGHTS) != 0;
+  constexpr bool kSc = !kMerge && (F & F_LIGHTS) != 0;
   [[maybe_unused]] double sps = 0.0, cps = 0.0;
   if constexpr (kSc) {
     const bool to_light = e0 < 0.5 && have_lights;
@@ -2178,7 +2070,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   double mat_pdf;
   if (lamb) {
     double ct = dot(unitv(gd), w);
-    mat_pdf = fmax(0.0, RT_MK_PI ? div_mk(ct, kPi, kInvPi) : ct / kPi);
+    mat_pdf = fmax(0.0, div_mk(ct, kPi, kInvPi));
   } else {
     mat_pdf = 1.0 / (4.0 * kPi);
   }
@@ -2194,7 +2086,7 @@ RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const K
   double spdf;
   if (lamb) {
     double ct = dot(h.n, unitv(gd));
-    spdf = ct < 0 ? 0 : (RT_MK_PI ? div_mk(ct, kPi, kInvPi) : ct / kPi);
+    spdf = ct < 0 ? 0 : div_mk(ct, kPi, kInvPi);
   } else {
     spdf = 1 / (4 * kPi);
   }

@@ -146,9 +146,9 @@ int rt_cpu_render(const rt_scene_desc *desc, const rt_frame *f, const rt_render_
   S.n_lds_nodes = S.n_nodes; // the walk reads every node from `lnodes`, in the staged form
   std::vector<DNodeL> lnodes_l;
   const DNode *lnodes = S.nodes;
-  if (RT_LDS_TRIPLE) {
+  {
     lnodes_l.reserve(H.nodes.size());
-    for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, RT_SLAB_FMA && RT_SLAB_SIGN));
+    for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, true));
     lnodes = (const DNode *)(const void *)lnodes_l.data();
   }
   const PixelFn fn = kPixelFns[S.features & (F_FLAT * 2 - 1)];

@@ -95,8 +95,8 @@ extern "C" int emu_render(const rt_scene_desc *desc, const rt_frame *f, const rt
   // in the form the kernel stages it: DNode4 as is, binary nodes as DNodeL
   std::vector<DNodeL> lnodes_l;
   const DNode *ln = S.nodes;
-  if (!bvh4 && RT_LDS_TRIPLE) {
-    for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, RT_SLAB_FMA && RT_SLAB_SIGN));
+  if (!bvh4) {
+    for (const DNode &nd : H.nodes) lnodes_l.push_back(lds_node(nd, true));
     ln = (const DNode *)(const void *)lnodes_l.data();
   }
   DCamera C;
