@@ -82,11 +82,20 @@ struct rt_scene {
   // cost-ordered dispatch ("tile order", launch()): per-tile unit costs of the
   // last launch and the two order buffers (the one a launch reads, the one the
   // sort after it writes for the next launch of the same shape)
-  uint32_t *tile_cost = nullptr;
-  int32_t *tile_order[2] = {nullptr, nullptr};
-  int order_cap = 0, order_cur = 0;
-  bool order_ready = false;
-  int32_t order_sig[10] = {};
+  // ... one slot per launch shape (signature), least recently used replaced:
+  // a scene that alternates tile subsets (several ranks' shares on one
+  // device) keeps an order for each instead of re-measuring one slot
+  struct OrderSlot {
+    uint32_t *tile_cost = nullptr;
+    int32_t *tile_order[2] = {nullptr, nullptr};
+    int cap = 0, cur = 0;
+    bool ready = false;
+    int32_t sig[10] = {};
+    uint64_t used = 0; // launch counter at the slot's last use
+  };
+  static constexpr int kOrderSlots = 4;
+  OrderSlot order[kOrderSlots];
+  uint64_t order_clock = 0;
   // caller streams rt_render_device launched on, each with an event recorded
   // after the scene's last work there (note_stream): destroy and buffer growth
   // wait on these and on the scene's own stream -- not on the whole device
@@ -571,9 +580,11 @@ int rt_scene_destroy(rt_scene *s) {
   if (s->stream) {
     scene_free(s, s->out_buf);
     scene_free(s, s->scratch);
-    scene_free(s, s->tile_cost);
-    scene_free(s, s->tile_order[0]);
-    scene_free(s, s->tile_order[1]);
+    for (auto &o : s->order) {
+      scene_free(s, o.tile_cost);
+      scene_free(s, o.tile_order[0]);
+      scene_free(s, o.tile_order[1]);
+    }
     scene_free(s, s->block);
     (void)hipStreamSynchronize(s->stream);
   }
@@ -750,19 +761,32 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
 // bit-identical with and without it (rt_tuning.no_tile_order,
 // tests/test_tile_order.py).  (Ordering across the split, so the cheapest
 // tiles became the tail, regrouped those tiles' sums: not bit-identical.)
-static int ensure_order(rt_scene *s, int n) {
-  if (s->order_cap >= n) return RT_OK;
-  if (s->tile_cost) wait_scene(s); // this scene's launches on any stream may still use them
-  scene_free(s, s->tile_cost);
-  scene_free(s, s->tile_order[0]);
-  scene_free(s, s->tile_order[1]);
-  s->order_cap = 0;
-  s->order_ready = false;
-  hipError_t e = scene_alloc(s, (void **)&s->tile_cost, (size_t)n * sizeof(uint32_t));
-  if (e == hipSuccess) e = scene_alloc(s, (void **)&s->tile_order[0], (size_t)n * sizeof(int32_t));
-  if (e == hipSuccess) e = scene_alloc(s, (void **)&s->tile_order[1], (size_t)n * sizeof(int32_t));
+// The slot of a launch shape: the one holding its signature, else the least
+// recently used (its order reset), with room for n tiles.
+static int order_slot(rt_scene *s, const int32_t sig[10], int n, rt_scene::OrderSlot *&slot) {
+  slot = nullptr;
+  for (auto &o : s->order)
+    if (o.ready && std::equal(sig, sig + 10, o.sig)) slot = &o;
+  if (!slot) {
+    slot = &s->order[0];
+    for (auto &o : s->order)
+      if (o.used < slot->used) slot = &o;
+    slot->ready = false;
+    std::copy(sig, sig + 10, slot->sig);
+  }
+  slot->used = ++s->order_clock;
+  if (slot->cap >= n) return RT_OK;
+  if (slot->tile_cost) wait_scene(s); // this scene's launches on any stream may still use them
+  scene_free(s, slot->tile_cost);
+  scene_free(s, slot->tile_order[0]);
+  scene_free(s, slot->tile_order[1]);
+  slot->cap = 0;
+  slot->ready = false;
+  hipError_t e = scene_alloc(s, (void **)&slot->tile_cost, (size_t)n * sizeof(uint32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[0], (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[1], (size_t)n * sizeof(int32_t));
   if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync tile order: ") + hipGetErrorString(e));
-  s->order_cap = n;
+  slot->cap = n;
   return RT_OK;
 }
 
@@ -805,14 +829,13 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
                        rtk_tile_order_f(s->ds.features);
   const int32_t sig[10] = {L.n_local_tiles, L.tile_first, L.tile_stride, L.tiles_x, L.row_begin,
                            L.row_end,       L.sample_count, sp.n_head,   sp.head_chunks, sp.chunks};
-  bool use_order = false;
+  rt_scene::OrderSlot *os = nullptr;
   if (ordered) {
-    int rc = ensure_order(s, L.n_local_tiles);
+    int rc = order_slot(s, sig, L.n_local_tiles, os);
     if (rc) return rc;
-    use_order = s->order_ready && std::equal(sig, sig + 10, s->order_sig);
-    Lp.tile_order = use_order ? s->tile_order[s->order_cur] : nullptr;
-    Lp.tile_cost = s->tile_cost;
-    hipError_t me = hipMemsetAsync(s->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
+    Lp.tile_order = os->ready ? os->tile_order[os->cur] : nullptr;
+    Lp.tile_cost = os->tile_cost;
+    hipError_t me = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
     if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
   } else {
     Lp.tile_order = nullptr;
@@ -838,14 +861,13 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   s->timed = true;
   if (ordered) { // the next launch's order, into the buffer this one did not read
-    const int next = s->order_cur ^ 1;
-    e = rtk_launch_tile_order(s->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
-                              s->tile_order[next], st);
+    const int next = os->cur ^ 1;
+    e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
+                              os->tile_order[next], st);
     if (e != hipSuccess) return hip_err(e, "tile order");
     if (order_used) *order_used = Lp.tile_order;
-    s->order_cur = next;
-    s->order_ready = true;
-    std::copy(sig, sig + 10, s->order_sig);
+    os->cur = next;
+    os->ready = true;
   }
   return RT_OK;
 }

@@ -78,3 +78,30 @@ def test_ordered_subsets_and_shards_equal_plan_order():
     with MultiRenderer(S, devices=(0,), shards=3) as M:
         for _ in range(3):
             assert np.array_equal(M.render(f, seed=7, output=abi.RT_OUT_SUM), one)
+
+
+def test_alternating_shapes_keep_their_own_orders():
+    """One scene launched round-robin over several tile subsets (ranks' shares
+    on one device, tools/shard_sim.py) keeps an order per launch shape (four
+    slots, least recently used replaced -- six shapes here, so slots are
+    evicted and re-measured): every frame still equals plan order bit for bit."""
+    S = load_scene(os.path.join(SCENES, "three_spheres.json"))
+    f = camera_frame(S.camera_desc(image_width=256, samples_per_pixel=64, max_depth=8))
+    world = 6
+    _, t_r = tile_counts(f, world)
+
+    def run(tune):
+        outs = []
+        with Renderer(S, tuning=tune) as R:
+            buf = torch.zeros((t_r, 64, 3), dtype=torch.float64, device="cuda")
+            for rnd in range(3):
+                for r in (list(range(world)) if rnd != 1 else [0, 1, 0, 1, 2, 0]):
+                    R.render_device(f, buf.data_ptr(), 0, seed=11, output=abi.RT_OUT_SUM,
+                                    accumulate=0, tiles=(r, world), layout=abi.RT_LAYOUT_TILES,
+                                    chunks=abi.RT_CHUNKS_AUTO)
+                    torch.cuda.synchronize()
+                    outs.append(buf.cpu().numpy().copy())
+        return outs
+
+    for x, y in zip(run(None), run({"no_tile_order": 1})):
+        assert np.array_equal(x, y)
