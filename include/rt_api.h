@@ -52,7 +52,13 @@
  * buffers, its work-unit counter (persistent launches) and its tile-cost /
  * dispatch-order buffers (rt_tuning.no_tile_order) are per scene.
  * Asynchronous launches (rt_render_device) on one scene must be ordered by the
- * caller's streams as any device work is.
+ * caller's streams as any device work is.  Destroying a scene, or a launch
+ * that grows its buffers, waits for that scene's own work only -- its stream
+ * and its last launch on each caller stream (an event per stream) -- never for
+ * other scenes' or threads' work on the device: scene memory is stream-ordered
+ * (hipMallocAsync / hipFreeAsync on the scene's stream), because a plain
+ * hipFree waits for the whole device.  Tile orders are kept per launch shape
+ * (four shapes per scene, least recently used replaced).
  *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
  * random stream is a stateless counter-based Philox4x32-10 keyed by
@@ -409,6 +415,8 @@ int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **scene)
 int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tuning *tuning,
                           rt_scene **scene);
 int rt_scene_info_get(const rt_scene *scene, rt_scene_info *info);
+/* Waits for the scene's own pending work (rt_render_device launches on any
+   caller stream included), then releases it; NULL is a no-op. */
 int rt_scene_destroy(rt_scene *scene);
 
 /* Render rows [row_begin,row_end) x strata [sample_begin, +sample_count) and

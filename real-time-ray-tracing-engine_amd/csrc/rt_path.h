@@ -1178,10 +1178,31 @@ RT_HD RT_FI void load_planes_l(NodePlanes<2> &pl, PS base, int node, const Plane
 // Both children of a binary node from their picked planes, verdicts returned
 // as two bools (an array of them made the compiler build the visit's branch
 // masks with VALU selects: C3 -1.6 %, profiles/r04g_c3_build_ab.log)
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0
+#endif
 RT_HD RT_FI void slab2_planes(const RayF<true> &q, const NodePlanes<2> &pl, float tmin32, float cl32,
                               float &t0, float &t1, bool &h0, bool &h1) {
   float th[2];
   float tl[2];
+#if defined(__HIP_DEVICE_COMPILE__) && RT_PK_SLAB
+  // both children's plane of an axis in one v_pk_fma_f32 (the pair the
+  // DNodeL read puts in adjacent registers): the same fma per plane, half
+  // the instructions
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 n[3], f[3];
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) {
+    const f2 inv = {q.inv[ax], q.inv[ax]}, mp = {-q.p[ax], -q.p[ax]};
+    n[ax] = __builtin_elementwise_fma(f2{pl.nr[ax][0], pl.nr[ax][1]}, inv, mp);
+    f[ax] = __builtin_elementwise_fma(f2{pl.fr[ax][0], pl.fr[ax][1]}, inv, mp);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    tl[c] = max3f(n[0][c], n[1][c], fmaxf(n[2][c], tmin32));
+    th[c] = min3f(f[0][c], f[1][c], min3f(f[2][c], cl32, cl32));
+  }
+#else
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const float ax = fmaf(pl.nr[0][c], q.inv[0], -q.p[0]), bx = fmaf(pl.fr[0][c], q.inv[0], -q.p[0]);
@@ -1190,6 +1211,7 @@ RT_HD RT_FI void slab2_planes(const RayF<true> &q, const NodePlanes<2> &pl, floa
     tl[c] = max3f(ax, ay, fmaxf(az, tmin32));
     th[c] = min3f(bx, by, min3f(bz, cl32, cl32));
   }
+#endif
   t0 = tl[0];
   t1 = tl[1];
   h0 = tl[0] <= fmaf(th[0], kSlabGrow, q.slack);

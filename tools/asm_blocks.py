@@ -5,7 +5,7 @@ walk (fp32 FMAs / LDS reads).   python tools/asm_blocks.py F [--pc (the 16-wave 
 import re
 import sys
 
-ASM = "real-time-ray-tracing-engine_amd/build/asm/rt_kernel-hip-amdgcn-amd-amdhsa-gfx950.s"
+ASM = __import__("os").environ.get("ASM", "real-time-ray-tracing-engine_amd/build/asm/rt_kernel-hip-amdgcn-amd-amdhsa-gfx950.s")
 
 
 def blocks(F, stats=0, pc=0):
