@@ -51,14 +51,16 @@
  * host thread at a time: its kernel-timing events, its scratch / staging
  * buffers, its work-unit counter (persistent launches) and its tile-cost /
  * dispatch-order buffers (rt_tuning.no_tile_order) are per scene.
- * Asynchronous launches (rt_render_device) on one scene must be ordered by the
- * caller's streams as any device work is.  Destroying a scene, or a launch
- * that grows its buffers, waits for that scene's own work only -- its stream
- * and its last launch on each caller stream (an event per stream) -- never for
- * other scenes' or threads' work on the device: scene memory is stream-ordered
- * (hipMallocAsync / hipFreeAsync on the scene's stream), because a plain
- * hipFree waits for the whole device.  Tile orders are kept per launch shape
- * (four shapes per scene, least recently used replaced).
+ * A scene's launches run one after another even on different caller streams:
+ * each launch waits for the scene's previous one (an event), since they share
+ * the scene's work-unit counter, scratch and tile orders; the caller orders
+ * its own buffers' producers and consumers with its streams as for any device
+ * work.  Destroying a scene, or a launch that grows its buffers, waits for
+ * that scene's own work only -- its stream and its last launch -- never for
+ * other scenes' or threads' work on the device: scene memory is
+ * stream-ordered (hipMallocAsync / hipFreeAsync on the scene's stream),
+ * because a plain hipFree waits for the whole device.  Tile orders are kept
+ * per launch shape (four shapes per scene, least recently used replaced).
  *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
  * random stream is a stateless counter-based Philox4x32-10 keyed by

@@ -96,10 +96,16 @@ struct rt_scene {
   static constexpr int kOrderSlots = 4;
   OrderSlot order[kOrderSlots];
   uint64_t order_clock = 0;
-  // caller streams rt_render_device launched on, each with an event recorded
-  // after the scene's last work there (note_stream): destroy and buffer growth
-  // wait on these and on the scene's own stream -- not on the whole device
-  std::vector<std::pair<hipStream_t, hipEvent_t>> used;
+  // The scene's launches form one chain across streams: `last` is recorded
+  // after each call's last kernel on its stream, and a launch on another
+  // stream first waits for it (order_after_last) -- the launches share the
+  // work-unit counter, the scratch and the order slots, so two of them must
+  // never overlap, whichever streams the caller passes.  The last launch's
+  // completion therefore implies all earlier ones': destroy and buffer growth
+  // wait for `last` and the scene's own stream -- not for the whole device.
+  hipEvent_t last = nullptr;
+  hipStream_t last_st = nullptr;
+  bool has_last = false;
 };
 
 namespace {
@@ -152,30 +158,24 @@ hipError_t upload(rt_scene *s, void *dst, const void *src, size_t bytes, hipMemc
   return e == hipSuccess ? hipStreamSynchronize(s->stream) : e;
 }
 // everything this scene has launched has completed: its own stream, and its
-// last launch on every caller stream
+// last launch (which every earlier launch precedes: order_after_last)
 void wait_scene(rt_scene *s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (auto &u : s->used) (void)hipEventSynchronize(u.second);
+  if (s->has_last) (void)hipEventSynchronize(s->last);
 }
-// after rt_render_device's work on caller stream st
-int note_stream(rt_scene *s, hipStream_t st) {
-  if (st == s->stream) return RT_OK;
-  auto it = std::find_if(s->used.begin(), s->used.end(), [&](const auto &u) { return u.first == st; });
-  if (it == s->used.end()) {
-    constexpr size_t kMaxStreams = 64; // a bound: the oldest stream's work is waited for and dropped
-    if (s->used.size() >= kMaxStreams) {
-      (void)hipEventSynchronize(s->used.front().second);
-      (void)hipEventDestroy(s->used.front().second);
-      s->used.erase(s->used.begin());
-    }
-    hipEvent_t ev;
-    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) return hip_err(e, "hipEventCreate");
-    s->used.emplace_back(st, ev);
-    it = s->used.end() - 1;
-  }
-  hipError_t e = hipEventRecord(it->second, st);
-  return e == hipSuccess ? RT_OK : hip_err(e, "hipEventRecord");
+// before a call's first kernel on st: after the scene's previous launch
+int order_after_last(rt_scene *s, hipStream_t st) {
+  if (!s->has_last || s->last_st == st) return RT_OK;
+  hipError_t e = hipStreamWaitEvent(st, s->last, 0);
+  return e == hipSuccess ? RT_OK : hip_err(e, "hipStreamWaitEvent");
+}
+// after a call's last kernel on st
+int mark_last(rt_scene *s, hipStream_t st) {
+  hipError_t e = hipEventRecord(s->last, st);
+  if (e != hipSuccess) return hip_err(e, "hipEventRecord");
+  s->last_st = st;
+  s->has_last = true;
+  return RT_OK;
 }
 
 // the shared launch validation (rt_scene.cpp; the CPU backend applies the same)
@@ -344,7 +344,8 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
   s->tune = tune;
   s->block_bytes = off;
   if ((e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess) {
+      (e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&s->last, hipEventDisableTiming)) != hipSuccess) {
     rt_scene_destroy(s);
     return hip_err(e, "stream/event create");
   }
@@ -588,7 +589,7 @@ int rt_scene_destroy(rt_scene *s) {
     scene_free(s, s->block);
     (void)hipStreamSynchronize(s->stream);
   }
-  for (auto &u : s->used) (void)hipEventDestroy(u.second);
+  if (s->last) (void)hipEventDestroy(s->last);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -829,6 +830,8 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
                        rtk_tile_order_f(s->ds.features);
   const int32_t sig[10] = {L.n_local_tiles, L.tile_first, L.tile_stride, L.tiles_x, L.row_begin,
                            L.row_end,       L.sample_count, sp.n_head,   sp.head_chunks, sp.chunks};
+  // after the scene's previous launch, whichever stream it ran on
+  if (int rc = order_after_last(s, st)) return rc;
   rt_scene::OrderSlot *os = nullptr;
   if (ordered) {
     int rc = order_slot(s, sig, L.n_local_tiles, os);
@@ -869,7 +872,7 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
     os->cur = next;
     os->ready = true;
   }
-  return RT_OK;
+  return mark_last(s, st);
 }
 
 static int ensure_out(rt_scene *s, size_t bytes) {
@@ -923,24 +926,17 @@ int rt_render_device(rt_scene *s, const rt_frame *f, const rt_render_params *p, 
   if ((rc = to_launch(f, &q, L))) return rc;
   DeviceGuard g(s->device);
   hipStream_t st = (hipStream_t)hip_stream; // NULL = the HIP null stream (HIP convention)
-  if (!auto_units) {
-    rc = launch(s, C, L, dev_rgb, nullptr, st);
-    const int rn = note_stream(s, st); // what destroy / buffer growth wait for
-    return rc ? rc : rn;
-  }
+  if (!auto_units) return launch(s, C, L, dev_rgb, nullptr, st);
   // the subset's own units: whole head tiles straight into dev_rgb, chunk
   // partials into the scratch, added in chunk order into dev_rgb (the
   // rt_multi shards' finish), all on `st`
   const SplitPlan sp = subset_plan(s, L);
   const int32_t *order = nullptr;
-  rc = launch(s, C, L, dev_rgb, nullptr, st, &sp, &order);
-  if (rc == RT_OK) {
-    hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
-                                           order, dev_rgb, st);
-    if (e != hipSuccess) rc = hip_err(e, "tile chunk sum");
-  }
-  const int rn = note_stream(s, st);
-  return rc ? rc : rn;
+  if ((rc = launch(s, C, L, dev_rgb, nullptr, st, &sp, &order))) return rc;
+  hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
+                                         order, dev_rgb, st);
+  if (e != hipSuccess) return hip_err(e, "tile chunk sum");
+  return mark_last(s, st); // the chunk sum reads the scratch: the chain ends after it
 }
 
 int rt_render_stats(rt_scene *s, const rt_frame *f, const rt_render_params *p,
@@ -1199,6 +1195,7 @@ static int render_shard(rt_scene *s, const rt_frame *f, const rt_render_params *
   if ((rc = launch(s, C, L, s->out_buf, nullptr, s->stream, &sp, &order))) return rc;
   hipError_t e = rtk_launch_shard_finish(s->scratch, L.n_local_tiles, sp.n_head, sp.head_chunks, sp.chunks,
                                          order, s->out_buf, s->stream);
+  if (e == hipSuccess && (rc = mark_last(s, s->stream))) return rc;
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return hip_err(e, "shard render");
   *t_done = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();

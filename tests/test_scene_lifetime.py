@@ -102,23 +102,57 @@ def test_destroy_right_after_an_async_launch_is_safe():
 
 
 def test_scenes_on_many_streams_and_buffer_growth():
-    """A scene used on several caller streams (and the null stream), with
-    growing launches that reallocate its scratch and tile-order buffers, renders
-    the same frames as a fresh scene; growth waits only for its own streams."""
+    """A scene used on several caller streams (and the null stream) in turn --
+    each launch ordered after the previous one by a stream wait, as the
+    threading contract asks (the launches of one scene share its work-unit
+    counter), but with no host synchronisation between them -- with growing
+    launches that reallocate its scratch and tile-order buffers while the
+    earlier launches may still run: the frames equal a fresh scene's."""
     import torch
     S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
     dev = torch.device("cuda", 0)
-    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    streams = [torch.cuda.Stream(dev) for _ in range(3)] + [torch.cuda.default_stream(dev)]
     with Renderer(S) as R:
         outs = []
+        prev = torch.cuda.current_stream(dev)
         for k, w in enumerate((64, 320, 960, 1920)):
             f = camera_frame(S.camera_desc(image_width=w, samples_per_pixel=64, max_depth=8))
-            o = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
-            sp = streams[k % 3].cuda_stream if k < 3 else 0
-            R.render_device(f, o.data_ptr(), sp, seed=k, output=abi.RT_OUT_SUM, accumulate=0)
+            st = streams[k]
+            with torch.cuda.stream(st):
+                o = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
+            st.wait_stream(prev)
+            R.render_device(f, o.data_ptr(), st.cuda_stream, seed=k, output=abi.RT_OUT_SUM,
+                            accumulate=0)
             outs.append((f, k, o))
+            prev = st
         torch.cuda.synchronize()
     with Renderer(S) as R2:
         for f, k, o in outs:
             want = R2.render(f, seed=k, output=abi.RT_OUT_SUM)
             assert np.array_equal(o.cpu().numpy(), want), f.image_width
+
+
+def test_launches_on_unordered_streams_are_chained():
+    """Launches of one scene on caller streams the caller did not order against
+    each other (here: two streams, no waits, persistent-instance frames that
+    share the scene's work-unit counter and scratch) run one after the other:
+    the library orders each launch after the scene's previous one, so every
+    frame equals a fresh scene's."""
+    import torch
+    S = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    f = camera_frame(S.camera_desc(image_width=960, samples_per_pixel=64, max_depth=8))
+    with Renderer(S) as R:
+        outs = []
+        for k in range(6):
+            st = streams[k % 2]
+            with torch.cuda.stream(st):
+                o = torch.empty((f.image_height, f.image_width, 3), dtype=torch.float64, device=dev)
+            R.render_device(f, o.data_ptr(), st.cuda_stream, seed=20 + k, output=abi.RT_OUT_SUM,
+                            accumulate=0)
+            outs.append(o)
+        torch.cuda.synchronize()
+    with Renderer(S) as R2:
+        for k, o in enumerate(outs):
+            assert np.array_equal(o.cpu().numpy(), R2.render(f, seed=20 + k, output=abi.RT_OUT_SUM)), k
