@@ -564,8 +564,11 @@ def progressive_rates(torch, dev, width=1920, frames=30):
       display_ms -- every frame also copies its 6.2 MB of bytes to pinned host
                     memory and waits for them (what a viewer must do per frame;
                     the reference copies the whole 49.8 MB fp64 accumulator back,
-                    DynamicCamera.cpp:524-532)."""
-    from rtx.progressive import for_renderer, frame_bytes
+                    DynamicCamera.cpp:524-532);
+      pipelined_display_ms -- the same bytes through rtx.progressive's
+                    DisplayPipeline: frame k's copy runs on a copy stream while
+                    frame k+1 renders, the viewer takes frame k-1's bytes."""
+    from rtx.progressive import DisplayPipeline, for_renderer, frame_bytes
     from rtx.render import Renderer, camera_frame
     from rtx.scene import load_scene
     res = {}
@@ -596,10 +599,25 @@ def progressive_rates(torch, dev, width=1920, frames=30):
                 host.copy_(out, non_blocking=True)
                 torch.cuda.current_stream(dev).synchronize()
             disp_ms = (time.perf_counter() - t0) * 1e3 / frames
+            pr.reset()
+            pipe = DisplayPipeline(pr)
+            for _ in range(2):  # warm
+                pipe.frame()
+                pipe.present()
+            pipe.flush()
+            pr.reset()
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                pipe.frame()
+                pipe.present()
+            pipe.flush()
+            pipe_ms = (time.perf_counter() - t0) * 1e3 / frames
         res[c] = {"scene": name, "width": f.image_width, "height": f.image_height,
                   "strata_per_frame": 1, "frames_to_converge": f.sqrt_spp ** 2,
                   "device_ms_per_frame": round(dev_ms, 3), "device_fps": round(1e3 / dev_ms, 1),
-                  "display_ms_per_frame": round(disp_ms, 3), "display_fps": round(1e3 / disp_ms, 1)}
+                  "display_ms_per_frame": round(disp_ms, 3), "display_fps": round(1e3 / disp_ms, 1),
+                  "pipelined_display_ms_per_frame": round(pipe_ms, 3),
+                  "pipelined_display_fps": round(1e3 / pipe_ms, 1)}
     return res
 
 

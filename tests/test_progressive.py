@@ -137,3 +137,36 @@ def test_adaptive_frames_follow_the_reference_thresholds():
         t[0] += 1 / 20.0
         ctl2.frame()                   # 20 fps: inside the band
     assert ctl2.strata == 2
+
+
+@pytest.mark.gpu
+def test_display_pipeline_bytes_equal_the_synchronous_loop():
+    """DisplayPipeline (frame k's bytes copied to pinned host memory while frame
+    k+1 renders): every presented frame is, byte for byte, the synchronous
+    loop's frame of the same index (render, quantise, copy, wait); present()
+    lags one frame, flush() gives the newest; frames past convergence re-send
+    the final image."""
+    from rtx.progressive import DisplayPipeline, for_renderer, frame_bytes
+    from rtx.render import Renderer
+    S = load_scene(SCENE)
+    f = camera_frame(S.camera_desc(image_width=96, samples_per_pixel=9, max_depth=8))
+    with Renderer(S) as R:
+        pr = for_renderer(R, f, seed=21)
+        want = []
+        for _ in range(11):  # 9 strata, then two frames of the converged image
+            pr.step()
+            want.append(frame_bytes(pr).cpu().numpy())
+        pipe = DisplayPipeline(for_renderer(R, f, seed=21), depth=3)
+        assert pipe.present() is None
+        got = []
+        for k in range(11):
+            pipe.frame()
+            p = pipe.present()
+            if k == 0:
+                assert p is None
+            else:
+                got.append(p.numpy().copy())
+        got.append(pipe.flush().numpy().copy())
+    assert len(got) == len(want)
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(g, w), k
