@@ -57,10 +57,13 @@
  * its own buffers' producers and consumers with its streams as for any device
  * work.  Destroying a scene, or a launch that grows its buffers, waits for
  * that scene's own work only -- its stream and its last launch -- never for
- * other scenes' or threads' work on the device: scene memory is
- * stream-ordered (hipMallocAsync / hipFreeAsync on the scene's stream),
- * because a plain hipFree waits for the whole device.  Tile orders are kept
- * per launch shape (four shapes per scene, least recently used replaced).
+ * other scenes' or threads' work on the device: scene memory comes from a
+ * library-owned pool per device (hipMallocFromPoolAsync on the scene's
+ * stream) because a plain hipFree waits for the whole device, and destroy
+ * queues nothing on any stream (a stream may share a hardware queue with a
+ * busy one): a destroyed scene's idle buffers are freed by the next
+ * allocation on the device, or at process exit.  Tile orders are kept per
+ * launch shape (four shapes per scene, least recently used replaced).
  *
  * Numerics.  All arithmetic is fp64, as in the reference (Vec3.hpp:184).  The
  * random stream is a stateless counter-based Philox4x32-10 keyed by

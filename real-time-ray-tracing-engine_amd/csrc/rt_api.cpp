@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -135,15 +136,77 @@ struct DeviceGuard { // restore the caller's current device
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Scene memory is stream-ordered: hipMallocAsync / hipFreeAsync on the scene's
-// own stream.  A plain hipFree -- and hipFreeAsync of hipMalloc'd memory --
+// Scene memory is stream-ordered: hipMallocFromPoolAsync / hipFreeAsync on the
+// scene's own stream.  A plain hipFree -- and hipFreeAsync of hipMalloc'd memory --
 // waits for every stream of the device (tools/free_probe.hip on gfx950: 300 ms
 // behind another stream's 300 ms kernel); hipFreeAsync of pool memory returns
 // at once.  So destroying or growing one scene waits only for that scene's own
 // work (wait_scene), never for other scenes or threads on the device.
+// The allocations come from the library's own pool on the scene's device,
+// which keeps freed memory reserved for the next scene or buffer (release
+// threshold UINT64_MAX): with the device's default pool (threshold 0) the
+// synchronisation after the frees handed the memory back to the system and
+// waited for the whole device to do so (tests/test_scene_lifetime.py: a
+// destroy waited out another scene's 300 ms render that way).
+hipMemPool_t scene_pool(int device) {
+  static std::mutex mu;
+  static std::vector<hipMemPool_t> pools;
+  std::lock_guard<std::mutex> lock(mu);
+  if ((int)pools.size() <= device) pools.resize(device + 1, nullptr);
+  if (!pools[device]) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) return nullptr;
+    uint64_t keep = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    pools[device] = pool;
+  }
+  return pools[device];
+}
+// A destroyed scene's buffers, idle (the destroy waited for the scene's last
+// launch) but not yet freed: destroy enqueues nothing on any stream, since a
+// HIP stream may share one of the device's few hardware queues
+// (GPU_MAX_HW_QUEUES) with another scene's busy stream, and anything queued
+// behind that stream's kernel -- a free, a synchronisation -- waits for it
+// (tests/test_scene_lifetime.py measured exactly that).  The next allocation
+// on the device frees them on its own stream, stream-ordered, before it
+// allocates; what no later allocation reaps is released at process exit.
+struct Graveyard {
+  std::mutex mu;
+  std::vector<std::pair<int, void *>> ptrs; // (device, pool allocation)
+};
+Graveyard &graveyard() {
+  static Graveyard *g = new Graveyard(); // never destroyed: usable from any static destructor
+  return *g;
+}
+template <class T>
+void bury(rt_scene *s, T *&p) {
+  if (p) {
+    Graveyard &g = graveyard();
+    std::lock_guard<std::mutex> lock(g.mu);
+    g.ptrs.emplace_back(s->device, (void *)p);
+  }
+  p = nullptr;
+}
+void reap(rt_scene *s) {
+  Graveyard &g = graveyard();
+  std::lock_guard<std::mutex> lock(g.mu);
+  auto keep = g.ptrs.begin();
+  for (auto &e : g.ptrs) {
+    if (e.first == s->device) (void)hipFreeAsync(e.second, s->stream);
+    else *keep++ = e;
+  }
+  g.ptrs.erase(keep, g.ptrs.end());
+}
 hipError_t scene_alloc(rt_scene *s, void **p, size_t bytes) {
   *p = nullptr;
-  hipError_t e = hipMallocAsync(p, std::max<size_t>(bytes, 1), s->stream);
+  reap(s); // earlier scenes' idle buffers back into the pool first
+  hipMemPool_t pool = scene_pool(s->device);
+  if (!pool) return hipErrorOutOfMemory;
+  hipError_t e = hipMallocFromPoolAsync(p, std::max<size_t>(bytes, 1), pool, s->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream); // usable from any stream from here on
   if (e != hipSuccess) *p = nullptr;
   return e;
@@ -352,7 +415,7 @@ int rt_scene_create_tuned(const rt_scene_desc *desc, int32_t device, const rt_tu
   e = scene_alloc(s, (void **)&s->block, off);
   if (e != hipSuccess) {
     rt_scene_destroy(s);
-    return set_err(RT_ERR_OOM, std::string("hipMallocAsync scene: ") + hipGetErrorString(e));
+    return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync scene: ") + hipGetErrorString(e));
   }
   for (const Part &p : parts)
     if (p.src && p.bytes) {
@@ -578,17 +641,16 @@ int rt_scene_destroy(rt_scene *s) {
   // work -- its stream and its last launch on each caller stream -- and no
   // other (stream-ordered frees, scene_alloc)
   wait_scene(s);
-  if (s->stream) {
-    scene_free(s, s->out_buf);
-    scene_free(s, s->scratch);
-    for (auto &o : s->order) {
-      scene_free(s, o.tile_cost);
-      scene_free(s, o.tile_order[0]);
-      scene_free(s, o.tile_order[1]);
-    }
-    scene_free(s, s->block);
-    (void)hipStreamSynchronize(s->stream);
+  // ... then hand its buffers to the graveyard (no stream operation here:
+  // see Graveyard)
+  bury(s, s->out_buf);
+  bury(s, s->scratch);
+  for (auto &o : s->order) {
+    bury(s, o.tile_cost);
+    bury(s, o.tile_order[0]);
+    bury(s, o.tile_order[1]);
   }
+  bury(s, s->block);
   if (s->last) (void)hipEventDestroy(s->last);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -740,7 +802,7 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
     s->scratch_bytes = 0;
   }
   hipError_t e = scene_alloc(s, (void **)&s->scratch, bytes);
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync scratch: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync scratch: ") + hipGetErrorString(e));
   s->scratch_bytes = bytes;
   return RT_OK;
 }
@@ -786,7 +848,7 @@ static int order_slot(rt_scene *s, const int32_t sig[10], int n, rt_scene::Order
   hipError_t e = scene_alloc(s, (void **)&slot->tile_cost, (size_t)n * sizeof(uint32_t));
   if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[0], (size_t)n * sizeof(int32_t));
   if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[1], (size_t)n * sizeof(int32_t));
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync tile order: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync tile order: ") + hipGetErrorString(e));
   slot->cap = n;
   return RT_OK;
 }
@@ -883,7 +945,7 @@ static int ensure_out(rt_scene *s, size_t bytes) {
     s->out_bytes = 0;
   }
   hipError_t e = scene_alloc(s, (void **)&s->out_buf, bytes);
-  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocAsync output: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync output: ") + hipGetErrorString(e));
   s->out_bytes = bytes;
   return RT_OK;
 }
@@ -1087,8 +1149,8 @@ int rt_multi_destroy(rt_multi *m) {
         DeviceGuard gs(s->device);
         (void)hipStreamSynchronize(s->stream);
       }
-    scene_free(m->scenes[0], m->stage); // stream-ordered on the root scene's stream
-    scene_free(m->scenes[0], m->frame);
+    bury(m->scenes[0], m->stage); // idle: every shard stream was synchronised above
+    bury(m->scenes[0], m->frame);
   }
   for (rt_scene *s : m->scenes) rt_scene_destroy(s);
   delete m;

@@ -32,7 +32,13 @@ def _long_frame(S, spp=1024):
 
 
 def test_destroy_does_not_wait_for_another_scenes_render():
+    import gc
     import torch
+    # earlier tests' garbage (pinned host tensors, streams) must not be freed
+    # inside the timed window: torch's pinned-memory free (hipHostFree) waits
+    # for the whole device, whatever the library does
+    gc.collect()
+    torch.cuda.synchronize()
     SB = load_scene(os.path.join(SCENES, "bouncing_seed42.json"))
     SA = load_scene(os.path.join(SCENES, "three_spheres.json"))
     fB = _long_frame(SB)
@@ -57,6 +63,7 @@ def test_destroy_does_not_wait_for_another_scenes_render():
                          accumulate=0)
         sA.synchronize()
         # B's long render in flight; A (idle) is destroyed from another thread
+        gc.disable()
         RB.render_device(fB, outB.data_ptr(), sB.cuda_stream, seed=4, output=abi.RT_OUT_SUM,
                          accumulate=0)
         took = {}
@@ -66,11 +73,14 @@ def test_destroy_does_not_wait_for_another_scenes_render():
             RA.close()
             took["ms"] = (time.perf_counter() - t) * 1e3
         th = threading.Thread(target=destroy_a)
-        t1 = time.perf_counter()
-        th.start()
-        th.join()
-        joined_ms = (time.perf_counter() - t1) * 1e3
-        b_done = not bool(sB.query())
+        try:
+            t1 = time.perf_counter()
+            th.start()
+            th.join()
+            joined_ms = (time.perf_counter() - t1) * 1e3
+            b_done = not bool(sB.query())
+        finally:
+            gc.enable()
         sB.synchronize()
     # A's destroy returned while B's render was still running
     assert took["ms"] < 0.3 * b_ms, (took, b_ms)

@@ -69,6 +69,45 @@ int main() {
     CK(hipEventDestroy(ev));
     std::printf("%-36s returned after %8.2f ms (spin kernel ended at %8.2f ms)\n", names[mode], t1 - t0, t2 - t0);
   }
+  // the whole release sequence of a scene while B's kernel runs: frees on A,
+  // then synchronise A, then destroy A's objects -- with the device's default
+  // pool (release threshold 0: a sync may hand freed memory back to the
+  // system) and with a pool that keeps its memory (threshold UINT64_MAX)
+  hipMemPool_t own;
+  hipMemPoolProps props = {};
+  props.allocType = hipMemAllocationTypePinned;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = 0;
+  CK(hipMemPoolCreate(&own, &props));
+  uint64_t keep = ~0ull;
+  CK(hipMemPoolSetAttribute(own, hipMemPoolAttrReleaseThreshold, &keep));
+  for (int mode = 0; mode < 2; ++mode) {
+    for (int rep = 0; rep < 3; ++rep) {
+      hipStream_t S;
+      CK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+      void *p[4];
+      for (int i = 0; i < 4; ++i) {
+        if (mode == 0) CK(hipMallocAsync(&p[i], (size_t)(64 + 32 * i) << 20, S));
+        else CK(hipMallocFromPoolAsync(&p[i], (size_t)(64 + 32 * i) << 20, own, S));
+      }
+      CK(hipMemsetAsync(p[0], 0, 1 << 20, S));
+      CK(hipStreamSynchronize(S));
+      hipLaunchKernelGGL(spin, dim3(8), dim3(64), 0, B, cycles, flag);
+      CK(hipGetLastError());
+      const double t0 = now_ms();
+      for (int i = 0; i < 4; ++i) CK(hipFreeAsync(p[i], S));
+      CK(hipStreamSynchronize(S));
+      const double t1 = now_ms();
+      CK(hipStreamDestroy(S));
+      const double t2 = now_ms();
+      CK(hipStreamSynchronize(B));
+      const double t3 = now_ms();
+      std::printf("%-36s rep %d: frees + sync %8.2f ms, stream destroy %8.2f ms (spin ended at %8.2f ms)\n",
+                  mode == 0 ? "default pool (threshold 0)" : "own pool (threshold max)", rep, t1 - t0,
+                  t2 - t1, t3 - t0);
+    }
+  }
+  CK(hipMemPoolDestroy(own));
   CK(hipFree(flag));
   CK(hipStreamDestroy(A));
   CK(hipStreamDestroy(B));
