@@ -52,6 +52,7 @@ extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double s
 extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
                                            hipStream_t stream);
 extern "C" int rtk_tile_order_f(int features);
+extern "C" int rtk_tile_cost_f(int features);
 extern "C" hipError_t rtk_launch_tile_order(const uint32_t *cost, int n, int n_head, int32_t *order,
                                             hipStream_t stream);
 extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
@@ -76,6 +77,8 @@ struct rt_scene {
   int32_t *unit_ctr = nullptr; // work-unit counter of persistent launches (scene block)
   double *scratch = nullptr; // chunk partials of chunked frame launches
   size_t scratch_bytes = 0;
+  double *probe_buf = nullptr; // output of the tile-order probe (tile_order_probe)
+  size_t probe_bytes = 0;
   int wave_slots = 0;        // resident waves of the render instance on this device
   int pc_grid = 0;           // resident blocks of the persistent instance on this device
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
@@ -645,6 +648,7 @@ int rt_scene_destroy(rt_scene *s) {
   // see Graveyard)
   bury(s, s->out_buf);
   bury(s, s->scratch);
+  bury(s, s->probe_buf);
   for (auto &o : s->order) {
     bury(s, o.tile_cost);
     bury(s, o.tile_order[0]);
@@ -853,6 +857,52 @@ static int order_slot(rt_scene *s, const int32_t sig[10], int n, rt_scene::Order
   return RT_OK;
 }
 
+// The order of a launch shape whose instance measures no tile costs (the rich
+// instances: the cost bookkeeping cost them 12.5 %, r05u_ab.log): one launch
+// of the STATS instance over the same tiles -- whole tiles of at most
+// kProbeStrata strata each, into a throwaway buffer -- adds each tile's
+// duration to the slot's cost counters, and the sort orders the plan's head
+// and tail tiles by them, as after a plain instance's own launch.  Once per
+// launch shape (order slot); the launches of the shape then take the order.
+static int tile_order_probe(rt_scene *s, const DCamera &C, const DLaunch &L, const SplitPlan &sp,
+                            rt_scene::OrderSlot *os, hipStream_t st) {
+  constexpr int kProbeStrata = 16; // r06u: 16 strata order C4 0.2 % better than 4
+  const size_t bytes = std::max<size_t>(1, (size_t)L.n_local_tiles * 64 * 3) * sizeof(double);
+  if (s->probe_bytes < bytes) {
+    if (s->probe_buf) wait_scene(s);
+    scene_free(s, s->probe_buf);
+    s->probe_bytes = 0;
+    hipError_t ae = scene_alloc(s, (void **)&s->probe_buf, bytes);
+    if (ae != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync probe: ") + hipGetErrorString(ae));
+    s->probe_bytes = bytes;
+  }
+  DLaunch Q = L;
+  Q.sample_count = std::min(L.sample_count, kProbeStrata);
+  Q.output = RT_OUT_SUM;
+  Q.accumulate = 0;
+  Q.compact = 1;
+  Q.n_head = L.n_local_tiles;
+  Q.head_chunks = 1;
+  Q.n_chunks = 1;
+  Q.chunk_strata = Q.sample_count;
+  Q.parts = nullptr;
+  Q.parts_final = 0;
+  Q.unit_ctr = nullptr;
+  Q.grid_cap = 0;
+  Q.tile_order = nullptr;
+  Q.tile_cost = os->tile_cost;
+  hipError_t e = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(s->stats, 0, RT_N_STATS * sizeof(unsigned long long), st);
+  if (e == hipSuccess) e = rtk_launch_render(&s->ds, &C, &Q, s->probe_buf, s->stats, st);
+  if (e == hipSuccess)
+    e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
+                              os->tile_order[os->cur ^ 1], st);
+  if (e != hipSuccess) return hip_err(e, "tile order probe");
+  os->cur ^= 1;
+  os->ready = true;
+  return RT_OK;
+}
+
 // forced: the split plan of a tile-layout launch whose whole tiles go to
 // dev_out (compact) and split tiles' raw partials to the scene's scratch
 // (rt_multi_render's shards, reproducing the one-device frame's units).
@@ -895,13 +945,19 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   // after the scene's previous launch, whichever stream it ran on
   if (int rc = order_after_last(s, st)) return rc;
   rt_scene::OrderSlot *os = nullptr;
+  // instances that measure their tiles' costs re-sort after every launch; the
+  // others take a probe's order once per shape
+  const bool kernel_costs = rtk_tile_cost_f(s->ds.features) != 0;
   if (ordered) {
     int rc = order_slot(s, sig, L.n_local_tiles, os);
     if (rc) return rc;
+    if (!kernel_costs && !os->ready && (rc = tile_order_probe(s, C, L, sp, os, st))) return rc;
     Lp.tile_order = os->ready ? os->tile_order[os->cur] : nullptr;
-    Lp.tile_cost = os->tile_cost;
-    hipError_t me = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
-    if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
+    Lp.tile_cost = kernel_costs ? os->tile_cost : nullptr;
+    if (kernel_costs) {
+      hipError_t me = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
+      if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
+    }
   } else {
     Lp.tile_order = nullptr;
     Lp.tile_cost = nullptr;
@@ -925,7 +981,8 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   e = hipEventRecord(s->ev1, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   s->timed = true;
-  if (ordered) { // the next launch's order, into the buffer this one did not read
+  if (ordered && !kernel_costs && order_used) *order_used = Lp.tile_order;
+  if (ordered && kernel_costs) { // the next launch's order, into the buffer this one did not read
     const int next = os->cur ^ 1;
     e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
                               os->tile_order[next], st);

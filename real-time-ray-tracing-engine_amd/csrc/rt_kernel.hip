@@ -190,7 +190,12 @@ __device__ __forceinline__ int order_tile(const DLaunch &L, int k) {
 // register-free start / end counters, r05z4_c4_order_ab.log).  rtk_tile_order_f mirrors it
 // for the host.
 #define RT_ORDER_F(F) ((F) == F_FLAT || ((F) & ~F_BVH4) == 0)
-extern "C" int rtk_tile_order_f(int features) { return RT_ORDER_F((unsigned)features) ? 1 : 0; }
+// Every instance takes a dispatch order (a scalar load per unit: C4 -0.5 %,
+// profiles/r06q_order_read_ab_C4.log); the rich ones get theirs from a short
+// probe launch of the STATS instance, which measures tile costs like the
+// plain ones (rt_api.cpp tile_order_probe).
+extern "C" int rtk_tile_order_f(int features) { return 1; }
+extern "C" int rtk_tile_cost_f(int features) { return RT_ORDER_F((unsigned)features) ? 1 : 0; }
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -357,8 +362,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   // the instances that take it: RT_ORDER_F); the unit's cost is its end time
   // minus its start time, both added to the tile's counter (mod 2^32), so no
   // start time is held across the path loop
-  if constexpr (RT_ORDER_F(F)) {
-    local_tile = order_tile(PU, local_tile);
+  local_tile = order_tile(PU, local_tile);
+  if constexpr (RT_ORDER_F(F) || STATS) {
     if (lane == 0 && PU.tile_cost != nullptr)
       atomicSub(&PU.tile_cost[local_tile], (unsigned)__builtin_amdgcn_s_memrealtime());
   }
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
       double *const ob = out_arg<PC || kEpiFresh>(out);
       const int part = unit - (PE.head_chunks == 1 ? PE.n_head : 0);
       double *o = to_parts ? PE.parts + 3 * ((size_t)part * 64 + lane)
-                  : PE.compact ? ob + 3 * ((size_t)(RT_ORDER_F(F) ? order_tile(PE, unit) : unit) * 64 + lane)
+                  : PE.compact ? ob + 3 * ((size_t)order_tile(PE, unit) * 64 + lane)
                                : ob + 3 * ((size_t)(j - PE.row_begin) * Ce.W + i);
       if (final_out && PE.accumulate) {
         o[0] += sx;
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   }
   __builtin_amdgcn_wave_barrier();
   // the unit's duration into its tile's cost (the next launch's dispatch order)
-  if constexpr (RT_ORDER_F(F)) {
+  if constexpr (RT_ORDER_F(F) || STATS) {
     if (lane == 0) {
       const DLaunch PT = launch_fields<true>(P);
       if (PT.tile_cost != nullptr)

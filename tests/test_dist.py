@@ -332,11 +332,11 @@ def _diag_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         S = load_scene(SCENE)
-        cam = S.camera_desc(image_width=16, samples_per_pixel=4, max_depth=4)
+        cam = S.camera_desc(image_width=16, samples_per_pixel=16, max_depth=4)
         acc = torch.zeros((9, 16, 3), dtype=torch.float64)
 
-        def launch_work(seed, b):  # rank 1 renders twice as much: a visible imbalance
-            for _ in range(1 + rank):
+        def launch_work(seed, b):  # rank 1 renders 4x as much: an imbalance CPU noise won't hide
+            for _ in range(1 + 3 * rank):
                 acc.copy_(torch.from_numpy(O.oracle_render(S, cam, O.MODE_COUNTER, seed,
                                                            output=abi.RT_OUT_SUM)))
 
@@ -363,6 +363,6 @@ def test_bench_rank_diagnostics_two_gloo_ranks(tmp_path):
     k = d["per_rank_kernel_ms"]
     assert len(k) == 2 and len(d["per_rank_exchange_ms"]) == 2
     assert d["kernel_ms_min"] == min(k) and d["kernel_ms_max"] == max(k)
-    assert k[1] > k[0]  # rank 1 did twice the work
+    assert k[1] > k[0]  # rank 1 did 4x the work
     # rank 0 finished first, so its exchange waits for rank 1's extra render
     assert d["exchange_ms_rank0"] > 0.3 * (k[1] - k[0])

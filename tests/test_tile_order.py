@@ -5,7 +5,9 @@ sums the same samples in the same order and chunk partials are added per tile
 in chunk order -- so every launch's frame equals, bit for bit, the frame of a
 scene that keeps plan order (rt_tuning.no_tile_order): frame launches (whole
 head tiles + chunked tail), the persistent instance, tile-subset launches with
-the library's units (RT_CHUNKS_AUTO) and rt_multi shards."""
+the library's units (RT_CHUNKS_AUTO) and rt_multi shards.  Instances that
+measure no tile costs themselves (the rich ones) take the order of one probe
+launch of the STATS instance per launch shape."""
 import os
 
 import numpy as np
@@ -32,7 +34,8 @@ def _frames(S, f, tune, seeds, **kw):
     ("three_spheres", 200, 16, {}),          # uniform split, every tile chunked
     ("bouncing_seed42", 320, 16, {}),        # persistent instance
     ("bouncing_seed42", 160, 16, {"grid_cap": 3}),
-    ("cornell_fog", 160, 16, {}),
+    ("cornell_fog", 160, 16, {}),            # rich instance: the order from a STATS probe
+    ("cornell_fog", 320, 64, {"head_strata": 64, "tail_tiles": 1, "tail_split": 4}),  # whole heads
 ])
 def test_ordered_frames_equal_plan_order_frames(name, width, spp, extra):
     S = load_scene(os.path.join(SCENES, name + ".json"))
