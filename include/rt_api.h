@@ -92,7 +92,8 @@ extern "C" {
    5: strata_chunks = RT_CHUNKS_AUTO (rt_render_device, RT_LAYOUT_TILES): the
       library's work units for a tile subset, per-tile sums out; rt_tuning
       sub_* and no_tile_order fields (in four of the reserved slots: same size
-      and offsets). */
+      and offsets); round 6: rt_tuning.probe_strata (a fifth reserved slot,
+      zero = the default, so version 5 callers are unaffected). */
 #define RT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
@@ -409,10 +410,13 @@ typedef struct rt_tuning {
   int32_t sub_head_strata;   /* strata per head unit; 0: 16 x sqrt(strata / 64) */
   int32_t sub_tail_split;    /* tail chunks per head chunk; 0: 2 */
   int32_t sub_tail_permille; /* tail tiles per 1000 wave slots; 0: 125; < 0: none */
-  int32_t no_tile_order;     /* 1: launches take their tiles in plan order (default: the previous
-                                launch's measured tile costs order them, most expensive first;
-                                the frames are the same bit for bit) */
-  int32_t reserved[3];
+  int32_t no_tile_order;     /* 1: launches take their tiles in plan order (default: a probe launch
+                                measures the tile costs once per launch shape and the launches of
+                                the shape take them most expensive first; the frames are the
+                                same bit for bit) */
+  int32_t probe_strata;      /* strata per pixel of the probe launch that measures a launch shape's
+                                tile costs for its dispatch order, once per shape; 0: 16 */
+  int32_t reserved[2];
 } rt_tuning;
 
 int rt_scene_create(const rt_scene_desc *desc, int32_t device, rt_scene **scene);

@@ -51,8 +51,6 @@ extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double s
                                           uint8_t *bytes, hipStream_t stream);
 extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
                                            hipStream_t stream);
-extern "C" int rtk_tile_order_f(int features);
-extern "C" int rtk_tile_cost_f(int features);
 extern "C" hipError_t rtk_launch_tile_order(const uint32_t *cost, int n, int n_head, int32_t *order,
                                             hipStream_t stream);
 extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
@@ -83,16 +81,15 @@ struct rt_scene {
   int pc_grid = 0;           // resident blocks of the persistent instance on this device
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
   rt_tuning tune{};          // explicit tuning (rt_scene_create_tuned; zero: the default plan)
-  // cost-ordered dispatch ("tile order", launch()): per-tile unit costs of the
-  // last launch and the two order buffers (the one a launch reads, the one the
-  // sort after it writes for the next launch of the same shape)
+  // cost-ordered dispatch ("tile order", launch()): per-tile unit costs
+  // measured by the shape's probe launch and the order sorted from them
   // ... one slot per launch shape (signature), least recently used replaced:
   // a scene that alternates tile subsets (several ranks' shares on one
-  // device) keeps an order for each instead of re-measuring one slot
+  // device) keeps an order for each instead of probing one slot again
   struct OrderSlot {
     uint32_t *tile_cost = nullptr;
-    int32_t *tile_order[2] = {nullptr, nullptr};
-    int cap = 0, cur = 0;
+    int32_t *tile_order = nullptr;
+    int cap = 0;
     bool ready = false;
     int32_t sig[10] = {};
     uint64_t used = 0; // launch counter at the slot's last use
@@ -651,8 +648,7 @@ int rt_scene_destroy(rt_scene *s) {
   bury(s, s->probe_buf);
   for (auto &o : s->order) {
     bury(s, o.tile_cost);
-    bury(s, o.tile_order[0]);
-    bury(s, o.tile_order[1]);
+    bury(s, o.tile_order);
   }
   bury(s, s->block);
   if (s->last) (void)hipEventDestroy(s->last);
@@ -817,11 +813,11 @@ static int ensure_scratch(rt_scene *s, size_t bytes) {
 // whatever tiles come last.  Tiles differ several-fold in cost (sky vs glass,
 // r05t: C2's units 0.2-2.5 ms at one device), and a costly tile met last
 // keeps its wave slot busy while the others idle: the one-device C2 frame
-// spent 7.7 % of its slot-time idle, an 8-way rank's share 14.5 %.  So each
-// launch measures its tiles' costs (units add their durations per tile) and a
-// one-block sort after it orders the tiles most expensive first for the next
-// launch of the same shape (longest processing time first): the plan's k-th
-// tile is then tile_order[k].  The head tiles are ordered among themselves and
+// spent 7.7 % of its slot-time idle, an 8-way rank's share 14.5 %.  So the
+// first launch of a shape is preceded by a probe that measures its tiles'
+// costs (tile_order_probe) and a one-block sort that orders the tiles most
+// expensive first (longest processing time first); every launch of the shape
+// takes that order: the plan's k-th tile is tile_order[k].  The head tiles are ordered among themselves and
 // the tail tiles among themselves (the tail still last), so every tile keeps
 // its own split into units -- whole, head chunks or tail chunks -- and so its
 // summation grouping: only the schedule moves, and the frames are
@@ -845,28 +841,29 @@ static int order_slot(rt_scene *s, const int32_t sig[10], int n, rt_scene::Order
   if (slot->cap >= n) return RT_OK;
   if (slot->tile_cost) wait_scene(s); // this scene's launches on any stream may still use them
   scene_free(s, slot->tile_cost);
-  scene_free(s, slot->tile_order[0]);
-  scene_free(s, slot->tile_order[1]);
+  scene_free(s, slot->tile_order);
   slot->cap = 0;
   slot->ready = false;
   hipError_t e = scene_alloc(s, (void **)&slot->tile_cost, (size_t)n * sizeof(uint32_t));
-  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[0], (size_t)n * sizeof(int32_t));
-  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[1], (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order, (size_t)n * sizeof(int32_t));
   if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync tile order: ") + hipGetErrorString(e));
   slot->cap = n;
   return RT_OK;
 }
 
-// The order of a launch shape whose instance measures no tile costs (the rich
-// instances: the cost bookkeeping cost them 12.5 %, r05u_ab.log): one launch
-// of the STATS instance over the same tiles -- whole tiles of at most
-// kProbeStrata strata each, into a throwaway buffer -- adds each tile's
-// duration to the slot's cost counters, and the sort orders the plan's head
-// and tail tiles by them, as after a plain instance's own launch.  Once per
-// launch shape (order slot); the launches of the shape then take the order.
+// The order of a launch shape: one launch of the STATS instance over the same
+// tiles -- whole tiles of at most kProbeStrata strata each (rt_tuning
+// probe_strata), into a scratch buffer -- adds each tile's duration to the
+// slot's cost counters, and the sort orders the plan's head and tail tiles by
+// them.  Once per launch shape (order slot); the launches of the shape then
+// take the order.  The render instances measure nothing themselves: the cost
+// bookkeeping compiled into them cost C4 12.5 % (r05u_ab.log) and C2 / C3 / C5
+// 0.9 % (r06y_ab_C*.log), while a once-per-shape order ranks the tiles as well
+// as one re-measured after every launch (r06x / r06y).
 static int tile_order_probe(rt_scene *s, const DCamera &C, const DLaunch &L, const SplitPlan &sp,
                             rt_scene::OrderSlot *os, hipStream_t st) {
-  constexpr int kProbeStrata = 16; // r06u: 16 strata order C4 0.2 % better than 4
+  // 16 strata: C4 +0.2 % over 4 (r06u), C2 +0.6 % / C3 +0.9 % over 4 and 1 (r06aa)
+  constexpr int kProbeStrata = 16;
   const size_t bytes = std::max<size_t>(1, (size_t)L.n_local_tiles * 64 * 3) * sizeof(double);
   if (s->probe_bytes < bytes) {
     if (s->probe_buf) wait_scene(s);
@@ -877,7 +874,7 @@ static int tile_order_probe(rt_scene *s, const DCamera &C, const DLaunch &L, con
     s->probe_bytes = bytes;
   }
   DLaunch Q = L;
-  Q.sample_count = std::min(L.sample_count, kProbeStrata);
+  Q.sample_count = std::min(L.sample_count, s->tune.probe_strata > 0 ? s->tune.probe_strata : kProbeStrata);
   Q.output = RT_OUT_SUM;
   Q.accumulate = 0;
   Q.compact = 1;
@@ -896,9 +893,8 @@ static int tile_order_probe(rt_scene *s, const DCamera &C, const DLaunch &L, con
   if (e == hipSuccess) e = rtk_launch_render(&s->ds, &C, &Q, s->probe_buf, s->stats, st);
   if (e == hipSuccess)
     e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
-                              os->tile_order[os->cur ^ 1], st);
+                              os->tile_order, st);
   if (e != hipSuccess) return hip_err(e, "tile order probe");
-  os->cur ^= 1;
   os->ready = true;
   return RT_OK;
 }
@@ -932,36 +928,25 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   }
   // cost-ordered dispatch: frame launches and forced / library plans, not the
   // STATS instance nor a caller's explicit chunk layout (its partials are the
-  // output, by plan tile)
-  // ... and launches long enough to pay for the cost memset and the sort: a
-  // progressive frame (one stratum per pixel, ~0.2 ms at 1080p) lost 8-10 %
-  // to them (profiles/r05z_bench_default.json vs r05r's)
-  constexpr int kOrderMinStrata = 16;
+  // output, by plan tile).  Progressive frames too (one stratum per pixel:
+  // C4 0.90 -> 0.81 ms per frame, C2 0.222 -> 0.212, r06aa_ab_progressive.log),
+  // now that the costs are measured once per shape, not by every launch.
   const bool ordered = !s->tune.no_tile_order && stats == nullptr && (forced || !L.parts_final) &&
-                       L.n_local_tiles > 1 && L.sample_count >= kOrderMinStrata &&
-                       rtk_tile_order_f(s->ds.features);
+                       L.n_local_tiles > 1;
   const int32_t sig[10] = {L.n_local_tiles, L.tile_first, L.tile_stride, L.tiles_x, L.row_begin,
                            L.row_end,       L.sample_count, sp.n_head,   sp.head_chunks, sp.chunks};
   // after the scene's previous launch, whichever stream it ran on
   if (int rc = order_after_last(s, st)) return rc;
   rt_scene::OrderSlot *os = nullptr;
-  // instances that measure their tiles' costs re-sort after every launch; the
-  // others take a probe's order once per shape
-  const bool kernel_costs = rtk_tile_cost_f(s->ds.features) != 0;
-  if (ordered) {
+  if (ordered) { // the shape's order, from a probe the first time
     int rc = order_slot(s, sig, L.n_local_tiles, os);
     if (rc) return rc;
-    if (!kernel_costs && !os->ready && (rc = tile_order_probe(s, C, L, sp, os, st))) return rc;
-    Lp.tile_order = os->ready ? os->tile_order[os->cur] : nullptr;
-    Lp.tile_cost = kernel_costs ? os->tile_cost : nullptr;
-    if (kernel_costs) {
-      hipError_t me = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
-      if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
-    }
+    if (!os->ready && (rc = tile_order_probe(s, C, L, sp, os, st))) return rc;
+    Lp.tile_order = os->tile_order;
   } else {
     Lp.tile_order = nullptr;
-    Lp.tile_cost = nullptr;
   }
+  Lp.tile_cost = nullptr;
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   if (forced) {
@@ -981,16 +966,7 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   e = hipEventRecord(s->ev1, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   s->timed = true;
-  if (ordered && !kernel_costs && order_used) *order_used = Lp.tile_order;
-  if (ordered && kernel_costs) { // the next launch's order, into the buffer this one did not read
-    const int next = os->cur ^ 1;
-    e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
-                              os->tile_order[next], st);
-    if (e != hipSuccess) return hip_err(e, "tile order");
-    if (order_used) *order_used = Lp.tile_order;
-    os->cur = next;
-    os->ready = true;
-  }
+  if (order_used) *order_used = Lp.tile_order;
   return mark_last(s, st);
 }
 

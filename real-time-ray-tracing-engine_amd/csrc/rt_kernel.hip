@@ -183,19 +183,12 @@ __device__ __forceinline__ int plan_tile(const DLaunch &L, int unit) {
 __device__ __forceinline__ int order_tile(const DLaunch &L, int k) {
   return L.tile_order != nullptr ? __builtin_amdgcn_readfirstlane(L.tile_order[k]) : k;
 }
-// the instances with cost-ordered dispatch (rt_api.cpp "tile order"): the
-// plain flat one (C2) and the plain BVH ones (C3, C5); in the rich instances
-// (C4) its bookkeeping costs registers the path loop needs (C4 -12.5 % for a
-// +1.4 % schedule gain, profiles/r05u_ab.log; -12.6 % again with the
-// register-free start / end counters, r05z4_c4_order_ab.log).  rtk_tile_order_f mirrors it
-// for the host.
-#define RT_ORDER_F(F) ((F) == F_FLAT || ((F) & ~F_BVH4) == 0)
-// Every instance takes a dispatch order (a scalar load per unit: C4 -0.5 %,
-// profiles/r06q_order_read_ab_C4.log); the rich ones get theirs from a short
-// probe launch of the STATS instance, which measures tile costs like the
-// plain ones (rt_api.cpp tile_order_probe).
-extern "C" int rtk_tile_order_f(int features) { return 1; }
-extern "C" int rtk_tile_cost_f(int features) { return RT_ORDER_F((unsigned)features) ? 1 : 0; }
+// Cost-ordered dispatch (rt_api.cpp "tile order"): every instance maps its
+// units through the launch's tile order (a scalar load per unit); only the
+// STATS instance measures tile costs, in the probe launch that orders a launch
+// shape once (rt_api.cpp tile_order_probe).  The cost bookkeeping compiled
+// into a render instance cost it registers and schedule even when skipped at
+// run time: C4 -12.5 % (r05u_ab.log), C2 / C3 / C5 -0.9 % (r06y_ab_C*.log).
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -358,12 +351,12 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     s_first = PU.sample_begin + chunk * cs;
     s_count = min(cs, PU.sample_count - chunk * cs);
   }
-  // the plan's k-th tile -> the launch's local tile (cost-ordered dispatch,
-  // the instances that take it: RT_ORDER_F); the unit's cost is its end time
-  // minus its start time, both added to the tile's counter (mod 2^32), so no
-  // start time is held across the path loop
+  // the plan's k-th tile -> the launch's local tile (cost-ordered dispatch);
+  // in the probe (STATS) the unit's cost is its end time minus its start time,
+  // both added to the tile's counter (mod 2^32), so no start time is held
+  // across the path loop
   local_tile = order_tile(PU, local_tile);
-  if constexpr (RT_ORDER_F(F) || STATS) {
+  if constexpr (STATS) {
     if (lane == 0 && PU.tile_cost != nullptr)
       atomicSub(&PU.tile_cost[local_tile], (unsigned)__builtin_amdgcn_s_memrealtime());
   }
@@ -482,8 +475,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
   }
   __builtin_amdgcn_wave_barrier();
-  // the unit's duration into its tile's cost (the next launch's dispatch order)
-  if constexpr (RT_ORDER_F(F) || STATS) {
+  // the unit's duration into its tile's cost (the probe: the shape's dispatch order)
+  if constexpr (STATS) {
     if (lane == 0) {
       const DLaunch PT = launch_fields<true>(P);
       if (PT.tile_cost != nullptr)

@@ -141,7 +141,7 @@ class Tuning(C.Structure):
                 ("extra_features", C.c_int32),
                 ("sub_head_strata", C.c_int32), ("sub_tail_split", C.c_int32),
                 ("sub_tail_permille", C.c_int32), ("no_tile_order", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("probe_strata", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 def tuning(t=None):

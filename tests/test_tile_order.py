@@ -1,13 +1,12 @@
-"""Cost-ordered dispatch (rt_api.cpp "tile order"): from the second launch of
-a shape on, a scene takes its tiles most expensive first, by the per-tile unit
-costs the previous launch measured.  Only the schedule moves -- every unit
-sums the same samples in the same order and chunk partials are added per tile
-in chunk order -- so every launch's frame equals, bit for bit, the frame of a
-scene that keeps plan order (rt_tuning.no_tile_order): frame launches (whole
-head tiles + chunked tail), the persistent instance, tile-subset launches with
-the library's units (RT_CHUNKS_AUTO) and rt_multi shards.  Instances that
-measure no tile costs themselves (the rich ones) take the order of one probe
-launch of the STATS instance per launch shape."""
+"""Cost-ordered dispatch (rt_api.cpp "tile order"): the first launch of a
+shape is preceded by one probe launch of the STATS instance that measures the
+tiles' costs, and every launch of the shape takes its tiles most expensive
+first by them.  Only the schedule moves -- every unit sums the same samples in
+the same order and chunk partials are added per tile in chunk order -- so every
+launch's frame equals, bit for bit, the frame of a scene that keeps plan order
+(rt_tuning.no_tile_order): frame launches (whole head tiles + chunked tail),
+the persistent instance, the rich instances, tile-subset launches with the
+library's units (RT_CHUNKS_AUTO) and rt_multi shards."""
 import os
 
 import numpy as np
@@ -34,13 +33,16 @@ def _frames(S, f, tune, seeds, **kw):
     ("three_spheres", 200, 16, {}),          # uniform split, every tile chunked
     ("bouncing_seed42", 320, 16, {}),        # persistent instance
     ("bouncing_seed42", 160, 16, {"grid_cap": 3}),
-    ("cornell_fog", 160, 16, {}),            # rich instance: the order from a STATS probe
+    ("three_spheres", 200, 16, {"probe_strata": 1}),  # a one-stratum probe
+    ("cornell_fog", 160, 16, {}),            # rich instance
+    ("cornell_fog", 320, 1, {}),             # one stratum per launch (a progressive frame)
+    ("three_spheres", 1920, 1, {}),
     ("cornell_fog", 320, 64, {"head_strata": 64, "tail_tiles": 1, "tail_split": 4}),  # whole heads
 ])
 def test_ordered_frames_equal_plan_order_frames(name, width, spp, extra):
     S = load_scene(os.path.join(SCENES, name + ".json"))
     f = camera_frame(S.camera_desc(image_width=width, samples_per_pixel=spp, max_depth=8))
-    seeds = [3, 3, 4, 3]  # the 2nd..4th launches run cost-ordered
+    seeds = [3, 3, 4, 3]  # every launch cost-ordered, the 1st after the shape's probe
     got = _frames(S, f, dict(extra), seeds)
     want = _frames(S, f, dict(extra, no_tile_order=1), seeds)
     for g, w in zip(got, want):
@@ -87,7 +89,7 @@ def test_alternating_shapes_keep_their_own_orders():
     """One scene launched round-robin over several tile subsets (ranks' shares
     on one device, tools/shard_sim.py) keeps an order per launch shape (four
     slots, least recently used replaced -- six shapes here, so slots are
-    evicted and re-measured): every frame still equals plan order bit for bit."""
+    evicted and probed again): every frame still equals plan order bit for bit."""
     S = load_scene(os.path.join(SCENES, "three_spheres.json"))
     f = camera_frame(S.camera_desc(image_width=256, samples_per_pixel=64, max_depth=8))
     world = 6
