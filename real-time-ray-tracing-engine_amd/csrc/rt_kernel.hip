@@ -244,8 +244,6 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
   // staged BVH prefix nodes [0, S.n_lds_nodes) (sizes: rtk_lds_bytes)
   extern __shared__ int4 dyn_lds[];
   __shared__ double acc_lds[BW][64][3];
-  // the unit's launch tile and start time (tile order / cost, rt_api.cpp):
-  // parked in LDS across the path loop instead of SGPRs
   // compacted leaf tests (BVH instances only; 1 KB per wave)
   __shared__ LeafPool leaf_pool[RT_LEAF_SHARE_F(F) ? BW : 1];
 
