@@ -51,6 +51,7 @@ extern "C" hipError_t rtk_launch_to_bytes(const double *rgb, int64_t n, double s
                                           uint8_t *bytes, hipStream_t stream);
 extern "C" hipError_t rtk_launch_tiles_sum(const double *parts, int64_t n_tiles, int chunks, double *out,
                                            hipStream_t stream);
+extern "C" int rtk_cost_f(int features);
 extern "C" hipError_t rtk_launch_tile_order(const uint32_t *cost, int n, int n_head, int32_t *order,
                                             hipStream_t stream);
 extern "C" hipError_t rtk_launch_shard_finish(const double *parts, int n_local, int n_head, int head_chunks,
@@ -82,14 +83,16 @@ struct rt_scene {
   double binary_cost = -1.0; // SAH cost of the binary tree when the device holds the 4-wide one
   rt_tuning tune{};          // explicit tuning (rt_scene_create_tuned; zero: the default plan)
   // cost-ordered dispatch ("tile order", launch()): per-tile unit costs
-  // measured by the shape's probe launch and the order sorted from them
+  // measured by the shape's probe launch (or, in the launches that measure
+  // their own, by the last launch) and two order buffers: the one a launch
+  // reads, the one the sort after a measuring launch writes for the next
   // ... one slot per launch shape (signature), least recently used replaced:
   // a scene that alternates tile subsets (several ranks' shares on one
   // device) keeps an order for each instead of probing one slot again
   struct OrderSlot {
     uint32_t *tile_cost = nullptr;
-    int32_t *tile_order = nullptr;
-    int cap = 0;
+    int32_t *tile_order[2] = {nullptr, nullptr};
+    int cap = 0, cur = 0;
     bool ready = false;
     int32_t sig[10] = {};
     uint64_t used = 0; // launch counter at the slot's last use
@@ -648,7 +651,8 @@ int rt_scene_destroy(rt_scene *s) {
   bury(s, s->probe_buf);
   for (auto &o : s->order) {
     bury(s, o.tile_cost);
-    bury(s, o.tile_order);
+    bury(s, o.tile_order[0]);
+    bury(s, o.tile_order[1]);
   }
   bury(s, s->block);
   if (s->last) (void)hipEventDestroy(s->last);
@@ -841,11 +845,13 @@ static int order_slot(rt_scene *s, const int32_t sig[10], int n, rt_scene::Order
   if (slot->cap >= n) return RT_OK;
   if (slot->tile_cost) wait_scene(s); // this scene's launches on any stream may still use them
   scene_free(s, slot->tile_cost);
-  scene_free(s, slot->tile_order);
+  scene_free(s, slot->tile_order[0]);
+  scene_free(s, slot->tile_order[1]);
   slot->cap = 0;
   slot->ready = false;
   hipError_t e = scene_alloc(s, (void **)&slot->tile_cost, (size_t)n * sizeof(uint32_t));
-  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order, (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[0], (size_t)n * sizeof(int32_t));
+  if (e == hipSuccess) e = scene_alloc(s, (void **)&slot->tile_order[1], (size_t)n * sizeof(int32_t));
   if (e != hipSuccess) return set_err(RT_ERR_OOM, std::string("hipMallocFromPoolAsync tile order: ") + hipGetErrorString(e));
   slot->cap = n;
   return RT_OK;
@@ -893,7 +899,7 @@ static int tile_order_probe(rt_scene *s, const DCamera &C, const DLaunch &L, con
   if (e == hipSuccess) e = rtk_launch_render(&s->ds, &C, &Q, s->probe_buf, s->stats, st);
   if (e == hipSuccess)
     e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
-                              os->tile_order, st);
+                              os->tile_order[os->cur], st);
   if (e != hipSuccess) return hip_err(e, "tile order probe");
   os->ready = true;
   return RT_OK;
@@ -938,15 +944,31 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   // after the scene's previous launch, whichever stream it ran on
   if (int rc = order_after_last(s, st)) return rc;
   rt_scene::OrderSlot *os = nullptr;
-  if (ordered) { // the shape's order, from a probe the first time
+  // The first tile-subset launch of a shape (a multi-GPU rank's share) in the
+  // flat world runs in plan order in the COST instance (rt_kernel.hip), which
+  // measures its own units, and the sort after it gives the order every later
+  // launch of the shape takes in the plain instance: an 8-way C2 share 0.81 ms
+  // against 0.85 with the probe's order or with costs re-measured after every
+  // launch (r06ag: an order measured under cost order itself ranks worse).
+  // Every other shape takes its probe's order.
+  // (Frame launches ordered this way measured the same as with the probe:
+  // r06ah_first_measure_frames_ab_C2.log.)
+  bool kernel_costs = ordered && forced != nullptr && rtk_cost_f(s->ds.features);
+  if (ordered) {
     int rc = order_slot(s, sig, L.n_local_tiles, os);
     if (rc) return rc;
-    if (!os->ready && (rc = tile_order_probe(s, C, L, sp, os, st))) return rc;
-    Lp.tile_order = os->tile_order;
+    if (os->ready) kernel_costs = false;
+    if (!kernel_costs && !os->ready && (rc = tile_order_probe(s, C, L, sp, os, st))) return rc;
+    Lp.tile_order = os->ready ? os->tile_order[os->cur] : nullptr;
   } else {
     Lp.tile_order = nullptr;
   }
   Lp.tile_cost = nullptr;
+  if (kernel_costs) {
+    hipError_t me = hipMemsetAsync(os->tile_cost, 0, (size_t)L.n_local_tiles * sizeof(uint32_t), st);
+    if (me != hipSuccess) return hip_err(me, "hipMemsetAsync tile cost");
+    Lp.tile_cost = os->tile_cost;
+  }
   hipError_t e = hipEventRecord(s->ev0, st);
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   if (forced) {
@@ -967,6 +989,14 @@ static int launch(rt_scene *s, const DCamera &C, const DLaunch &L, double *dev_o
   if (e != hipSuccess) return hip_err(e, "hipEventRecord");
   s->timed = true;
   if (order_used) *order_used = Lp.tile_order;
+  if (kernel_costs) { // the next launch's order, into the buffer this one did not read
+    const int next = os->cur ^ 1;
+    e = rtk_launch_tile_order(os->tile_cost, L.n_local_tiles, std::min(sp.n_head, L.n_local_tiles),
+                              os->tile_order[next], st);
+    if (e != hipSuccess) return hip_err(e, "tile order");
+    os->cur = next;
+    os->ready = true;
+  }
   return mark_last(s, st);
 }
 

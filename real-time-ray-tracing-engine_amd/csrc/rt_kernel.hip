@@ -184,11 +184,17 @@ __device__ __forceinline__ int order_tile(const DLaunch &L, int k) {
   return L.tile_order != nullptr ? __builtin_amdgcn_readfirstlane(L.tile_order[k]) : k;
 }
 // Cost-ordered dispatch (rt_api.cpp "tile order"): every instance maps its
-// units through the launch's tile order (a scalar load per unit); only the
-// STATS instance measures tile costs, in the probe launch that orders a launch
+// units through the launch's tile order (a scalar load per unit); the STATS
+// instance measures tile costs, in the probe launch that orders a launch
 // shape once (rt_api.cpp tile_order_probe).  The cost bookkeeping compiled
 // into a render instance cost it registers and schedule even when skipped at
-// run time: C4 -12.5 % (r05u_ab.log), C2 / C3 / C5 -0.9 % (r06y_ab_C*.log).
+// run time: C4 -12.5 % (r05u_ab.log), C2 / C3 / C5 -0.9 % (r06y_ab_C*.log);
+// so it lives in one extra instance (COST) of the flat world only, for the
+// tile-subset launches of a multi-GPU rank, whose order re-measured after
+// every launch beats the probe's (r06ad / r06af: 8-way C2 share).
+// rtk_cost_f mirrors it for the host.
+#define RT_COST_F(F) ((F) == F_FLAT)
+extern "C" int rtk_cost_f(int features) { return RT_COST_F((unsigned)features) ? 1 : 0; }
 template <bool FRESH>
 __device__ __forceinline__ double *out_arg(double *out) {
   if constexpr (FRESH) {
@@ -232,7 +238,7 @@ extern "C" hipError_t rtk_unit_times_clear(void) {
 // PCW: 0 = one work unit per wavefront; else a persistent instance with
 // blocks of PCW waves (kPcWaves = one block per CU; kWaves when the traversal
 // stacks of 16 waves do not fit the CU's LDS, e.g. deep 4-wide trees)
-template <bool STATS, unsigned F, int PCW = 0>
+template <bool STATS, unsigned F, int PCW = 0, bool COST = false>
 __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(F)))) void render_tiles(DScene S_, DCamera C, DLaunch P, double *out,
                                                     unsigned long long *stats) {
   constexpr bool PC = PCW > 0;
@@ -350,11 +356,11 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     s_count = min(cs, PU.sample_count - chunk * cs);
   }
   // the plan's k-th tile -> the launch's local tile (cost-ordered dispatch);
-  // in the probe (STATS) the unit's cost is its end time minus its start time,
-  // both added to the tile's counter (mod 2^32), so no start time is held
-  // across the path loop
+  // in the probe (STATS) and the COST instance the unit's cost is its end time
+  // minus its start time, both added to the tile's counter (mod 2^32), so no
+  // start time is held across the path loop
   local_tile = order_tile(PU, local_tile);
-  if constexpr (STATS) {
+  if constexpr (STATS || COST) {
     if (lane == 0 && PU.tile_cost != nullptr)
       atomicSub(&PU.tile_cost[local_tile], (unsigned)__builtin_amdgcn_s_memrealtime());
   }
@@ -473,8 +479,8 @@ __global__ __launch_bounds__(64 * (PCW ? PCW : block_waves(F))) __attribute__((a
     }
   }
   __builtin_amdgcn_wave_barrier();
-  // the unit's duration into its tile's cost (the probe: the shape's dispatch order)
-  if constexpr (STATS) {
+  // the unit's duration into its tile's cost (the shape's dispatch order)
+  if constexpr (STATS || COST) {
     if (lane == 0) {
       const DLaunch PT = launch_fields<true>(P);
       if (PT.tile_cost != nullptr)
@@ -669,6 +675,11 @@ RenderFn persistent_instance(unsigned f, int pcw) {
   return (f & F_BVH4) ? render_tiles<false, F_BVH4, kWaves> : render_tiles<false, 0u, kWaves>;
 }
 
+// the cost-measuring instance (RT_COST_F: the flat world, never persistent);
+// the plain BVH worlds' shares measured as well as by the probe (C3 4- / 8-way
+// shares +-0.2 %, profiles/r06ai_sim_C3.log), so they have none
+RenderFn cost_instance(unsigned f) { return f == F_FLAT ? render_tiles<false, F_FLAT, 0, true> : nullptr; }
+
 // one instance per feature set (F_MEDIA | F_XFORM | F_LIGHTS | F_NOISE | F_FLAT)
 const RenderFn *render_table(bool stats) {
   static constexpr auto plain = instance_table<false>(std::make_integer_sequence<unsigned, F_ALL + 1>{});
@@ -788,6 +799,13 @@ extern "C" hipError_t rtk_launch_render(const DScene *S, const DCamera *C, const
   int blocks = (int)((units + bw - 1) / bw);
   if (blocks == 0) return hipSuccess;
   RenderFn fn = render_table(stats != nullptr)[S->features & F_ALL];
+  // a launch that measures its tiles' costs (rt_api.cpp: the first tile-subset
+  // launch of a shape in the flat world)
+  const bool cost = stats == nullptr && P->tile_cost != nullptr;
+  if (cost) {
+    fn = cost_instance((unsigned)(S->features & F_ALL));
+    if (fn == nullptr) return hipErrorInvalidValue;
+  }
   size_t lds = rtk_lds_bytes(S->features, S->stack_depth, S->n_lds_nodes);
   int launch_waves = bw;
   DLaunch Q = *P;

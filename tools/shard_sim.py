@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--tuning", nargs="+", default=[None],
                     help="rt_tuning dicts as JSON (one scene per entry), e.g. "
                          "'{\"sub_head_strata\": 32}'")
+    ap.add_argument("--settle", type=int, default=1,
+                    help="untimed launches of a share before its timed one (a rank's steady state)")
     ap.add_argument("--strata-sharding", action="store_true",
                     help="also time the stratum-sharded split")
     a = ap.parse_args()
@@ -112,7 +114,8 @@ def case(a, R, f, frame, strata, t1, N, U):
     per_rank = [None] * N
     for _ in range(a.reps):
         for r in (range(N) if a.rank_order == "fwd" else range(N - 1, -1, -1)):
-            share(r)
+            for _ in range(a.settle):
+                share(r)
             t = timed(lambda: share(r), 1)  # render + chunk sum
             per_rank[r] = t if per_rank[r] is None else min(per_rank[r], t)
     t_frame = timed(lambda: device_tiles_to_frame(gath, f, frame), a.reps)
@@ -130,7 +133,7 @@ def case(a, R, f, frame, strata, t1, N, U):
         "gather_bytes_per_rank": gbytes, "gather_ms": round(gather, 3),
         "speedup_k": round(t1 / (tiles_max + gather / a.k), 2),
         "rank0_path_trip_lane_use": round(st0["segments"] / max(1, 64 * st0["wave_trips"]), 4),
-        "rank_order": a.rank_order}
+        "rank_order": a.rank_order, "settle": a.settle}
     if a.rank_work:
         sts = [st0] + [R.stats(f, seed=0, tiles=(r, N), layout=abi.RT_LAYOUT_TILES, chunks=ch)
                        for r in range(1, N)]
