@@ -1905,6 +1905,7 @@ RT_HD RT_FI bool advance(PathState &ps, const DCamera &C) {
 // Measured (profiles/r02w_shade_merge_ab.log): C3 (plain BVH instance, mixed
 // Lambertian / metal / glass) +2 %; C2 (flat, Lambertian only: the selects are
 // pure overhead) -2 %, C4 -1 % (more spills): merged in the plain BVH instances only.
+// Re-measured on the round-6 build (profiles/r06am_*): C2 -2.9 %, C4 -2.4 %.
 #define RT_SHADE_MERGE_F(F) (((F) & ~F_BVH4) == 0)
 template <bool STATS, unsigned F>
 RT_HD RT_FI bool shade(const DScene &S, const DCamera &C, PathState &ps, const Key &key,
