@@ -8,9 +8,10 @@ import sys
 ASM = __import__("os").environ.get("ASM", "real-time-ray-tracing-engine_amd/build/asm/rt_kernel-hip-amdgcn-amd-amdhsa-gfx950.s")
 
 
-def blocks(F, stats=0, pc=0):
+def blocks(F, stats=0, pc=0, cost=0):
     s = open(ASM).read()
-    name = "_ZN12_GLOBAL__N_112render_tilesILb%dELj%dELi%dEEEv6DScene7DCamera7DLaunchPdPy" % (stats, F, pc)
+    # render_tiles<STATS, F, PCW, COST> (COST: the flat world's cost-measuring instance)
+    name = "_ZN12_GLOBAL__N_112render_tilesILb%dELj%dELi%dELb%dEEEv6DScene7DCamera7DLaunchPdPy" % (stats, F, pc, cost)
     i = s.index(name + ":")
     j = s.index(".Lfunc_end", i)
     out, cur = [], ["entry", []]

@@ -18,9 +18,9 @@ for line in t.splitlines():
         rows[cur][m.group(1)] = int(m.group(2))
 want = set(int(a) for a in sys.argv[1:])
 for k, v in rows.items():
-    m = re.search(r"render_tilesILb(\d)ELj(\d+)ELi(\d+)E", k)
+    m = re.search(r"render_tilesILb(\d)ELj(\d+)ELi(\d+)ELb(\d)E", k)
     if not m or (want and int(m.group(2)) not in want):
         continue
-    print("STATS=%s F=%-2s PC=%-2s VGPR %3s SGPR %3s spillV %3s spillS %3s occ %s scratch %s" % (
-        m.group(1), m.group(2), m.group(3), v.get("VGPRs"), v.get("SGPRs"), v.get("VGPRs Spill"),
+    print("STATS=%s F=%-2s PC=%-2s COST=%s VGPR %3s SGPR %3s spillV %3s spillS %3s occ %s scratch %s" % (
+        m.group(1), m.group(2), m.group(3), m.group(4), v.get("VGPRs"), v.get("SGPRs"), v.get("VGPRs Spill"),
         v.get("SGPRs Spill"), v.get("Occupancy [waves/SIMD]"), v.get("ScratchSize [bytes/lane]")))
